@@ -1,0 +1,93 @@
+"""ctypes binding of liboctsam_hip.so (the C ABI declared in include/octsam.h).
+
+The library is loaded after ``torch`` so that the HIP runtime torch already mapped
+(libamdhip64.so.7) is the one the library binds to: one runtime, one set of streams.
+There is no fallback: if the library or a GPU is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboctsam_hip.so")
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+
+c_void_p = ctypes.c_void_p
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p), ("B", c_void_p), ("C", c_void_p), ("bias", c_void_p), ("R", c_void_p),
+        ("C_pre", c_void_p), ("row_map", c_void_p), ("A2", c_void_p), ("B2", c_void_p),
+        ("M", c_int32), ("N", c_int32), ("K", c_int32), ("batch", c_int32),
+        ("lda", c_int64), ("ldb", c_int64), ("ldc", c_int64), ("ldr", c_int64),
+        ("stride_a", c_int64), ("stride_b", c_int64), ("stride_c", c_int64), ("stride_r", c_int64),
+        ("alpha", c_float), ("beta", c_float),
+        ("act", c_int32), ("a_mode", c_int32), ("b_mode", c_int32),
+        ("c_f32", c_int32), ("r_f32", c_int32), ("pre_f32", c_int32), ("conv_c", c_int32),
+        ("a2_rows", c_int32), ("b2_rows", c_int32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol here is declared in include/octsam.h
+_SIGNATURES = {
+    "octsam_abi_version": (c_int32, []),
+    "octsam_last_error": (ctypes.c_char_p, []),
+    "octsam_gemm": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
+    "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
+    "octsam_cubical_ph": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+class OctsamError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the shared library (no GPU needed). Raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OctsamError(f"liboctsam_hip.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def symbols() -> list[str]:
+    return list(_SIGNATURES)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().octsam_last_error().decode(errors="replace")
+        raise OctsamError(f"{what} failed (code {rc}): {msg}")
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args) -> None:
+    """Call a C-ABI entry point whose last argument is the stream; raise on error."""
+    fn = getattr(load(), name)
+    rc = fn(*args, c_void_p(stream_handle()))
+    check(rc, name)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()

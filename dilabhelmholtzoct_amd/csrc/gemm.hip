@@ -1,0 +1,373 @@
+// MFMA bf16 GEMM for gfx950 with fused epilogues and implicit-GEMM operand loaders.
+//
+//   C[b][m][n] = epi( alpha * sum_k A[b][m][k] * B[b][n][k] )          (fp32 accumulate)
+//
+// A operand modes (template AM):
+//   0  row-major  A[m*lda + k]                     (Linear input, K contiguous)
+//   1  transposed A[k*lda + m]                     (dY^T for weight gradients)
+//   2  patch16    A from fp32 NCHW pixels          (SamPatchEmbeddings conv 16x16/s16 as im2col,
+//                                                   hf modeling_sam.py:116-129)
+//   3  conv3x3    A from bf16 NHWC 64x64 map, k = (ky*3+kx)*C + c, zero padding 1
+//                                                  (SamVisionNeck.conv2, modeling_sam.py:985-992)
+//   4  row-major plus a row-periodic addend A2[(m % a2_rows)*lda + k]   (keys + key_pe,
+//                                                  SamTwoWayAttentionBlock, modeling_sam.py:327-343)
+// B operand modes (template BMODE):
+//   0  B[n*ldb + k]   (nn.Linear weight [out,in])
+//   1  B[k*ldb + n]   (weight used transposed, activations for dW)
+//   2  like 1 plus B2[(k % b2_rows)*ldb + n]       (dW of a product whose input was keys + key_pe)
+//
+// Epilogue (runtime): v = alpha*acc (+ beta*C_old) (+ bias[n]) -> act -> (+ residual) ; optional
+// pre-activation store; optional output row remap (window unpartition: drop padded tokens).
+//
+// Tiling: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 via 2x2 v_mfma_f32_32x32x16_bf16.
+// LDS image [row][64] bf16 with the 16-byte chunk index XOR-swizzled by ((row>>1)&7) so that the
+// ds_read_b128 lane groups of the 32x32x16 fragment reads are conflict-free.
+// Register-staged double buffer, one barrier per K-step; XCD-aware block remap so that the tiles
+// of one A row-panel run on one XCD (shared L2).
+#include "common.h"
+#include "../../include/octsam.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+
+struct GemmK {
+  const void* A;
+  const void* B;
+  void* C;
+  const float* bias;
+  const void* R;
+  void* Cpre;
+  const int* row_map;
+  const void* A2;
+  const void* B2;
+  int a2_rows, b2_rows;
+  int M, N, K;
+  long long lda, ldb, ldc, ldr;
+  long long sA, sB, sC, sR;
+  float alpha, beta;
+  int act;
+  int c_f32, r_f32, pre_f32;
+  int conv_c;  // channels for conv3x3 mode
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ int lds_idx(int r, int c) {  // bf16 element index in a [rows][64] image
+  return r * BK + ((c ^ ((r >> 1) & 7)) << 3);
+}
+
+__device__ __forceinline__ bf16x8 cvt8(const float4 a, const float4 b) {
+  bf16x8 r;
+  r[0] = (bf16)a.x; r[1] = (bf16)a.y; r[2] = (bf16)a.z; r[3] = (bf16)a.w;
+  r[4] = (bf16)b.x; r[5] = (bf16)b.y; r[6] = (bf16)b.z; r[7] = (bf16)b.w;
+  return r;
+}
+
+// Stage: each thread holds 4 chunks of 8 bf16 for the operand tile (128 rows x 64 k).
+template <int MODE>
+struct Loader {
+  bf16x8 v[4];
+
+  __device__ __forceinline__ void load(const GemmK& p, const void* base, const void* add, int period,
+                                       long long ld, int rows, int row0, int k0, int tid) {
+    if constexpr (MODE == 4) {
+      const bf16* src = (const bf16*)base;
+      const bf16* ad = (const bf16*)add;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int r = ci >> 3, c = ci & 7;
+        int gr = row0 + r, gk = k0 + c * 8;
+        if (gr < rows && gk < p.K) {
+          bf16x8 x = *(const bf16x8*)(src + (long long)gr * ld + gk);
+          bf16x8 y = *(const bf16x8*)(ad + (long long)(gr % period) * ld + gk);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
+          v[i] = x;
+        } else {
+          v[i] = (bf16x8)(bf16)0.0f;
+        }
+      }
+    } else if constexpr (MODE == 5) {  // B mode 2: transposed plus k-periodic addend
+      const bf16* src = (const bf16*)base;
+      const bf16* ad = (const bf16*)add;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int k = ci >> 4, rc = ci & 15;
+        int gr = row0 + rc * 8, gk = k0 + k;
+        if (gr < rows && gk < p.K) {
+          bf16x8 x = *(const bf16x8*)(src + (long long)gk * ld + gr);
+          bf16x8 y = *(const bf16x8*)(ad + (long long)(gk % period) * ld + gr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
+          v[i] = x;
+        } else {
+          v[i] = (bf16x8)(bf16)0.0f;
+        }
+      }
+    } else if constexpr (MODE == 0) {
+      const bf16* src = (const bf16*)base;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int r = ci >> 3, c = ci & 7;
+        int gr = row0 + r, gk = k0 + c * 8;
+        if (gr < rows && gk < p.K)
+          v[i] = *(const bf16x8*)(src + (long long)gr * ld + gk);
+        else
+          v[i] = (bf16x8)(bf16)0.0f;
+      }
+    } else if constexpr (MODE == 1) {
+      const bf16* src = (const bf16*)base;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int k = ci >> 4, rc = ci & 15;
+        int gr = row0 + rc * 8, gk = k0 + k;
+        if (gr < rows && gk < p.K)
+          v[i] = *(const bf16x8*)(src + (long long)gk * ld + gr);
+        else
+          v[i] = (bf16x8)(bf16)0.0f;
+      }
+    } else if constexpr (MODE == 2) {
+      const float* px = (const float*)base;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int r = ci >> 3, c = ci & 7;
+        int gr = row0 + r, gk = k0 + c * 8;
+        if (gr < rows && gk < p.K) {
+          int b = gr >> 12, ph = (gr >> 6) & 63, pw = gr & 63;
+          int ch = gk >> 8, kh = (gk >> 4) & 15, kw = gk & 15;
+          const float* s = px + (((long long)(b * 3 + ch) * 1024 + ph * 16 + kh) * 1024 + pw * 16 + kw);
+          float4 a0 = *(const float4*)s;
+          float4 a1 = *(const float4*)(s + 4);
+          v[i] = cvt8(a0, a1);
+        } else {
+          v[i] = (bf16x8)(bf16)0.0f;
+        }
+      }
+    } else {  // MODE 3: conv3x3 over NHWC 64x64 bf16
+      const bf16* src = (const bf16*)base;
+      const int C = p.conv_c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int r = ci >> 3, c = ci & 7;
+        int gr = row0 + r, gk = k0 + c * 8;
+        bf16x8 val = (bf16x8)(bf16)0.0f;
+        if (gr < rows && gk < p.K) {
+          int b = gr >> 12, y = (gr >> 6) & 63, x = gr & 63;
+          int tap = gk / C, ch = gk - tap * C;
+          int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+          if (yy >= 0 && yy < 64 && xx >= 0 && xx < 64)
+            val = *(const bf16x8*)(src + (((long long)b * 64 + yy) * 64 + xx) * C + ch);
+        }
+        v[i] = val;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(bf16* lds, int tid) {
+    if constexpr (MODE == 1 || MODE == 5) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int k = ci >> 4, rc = ci & 15;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          int r = rc * 8 + e;
+          lds[lds_idx(r, k >> 3) + (k & 7)] = v[i][e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ci = tid + i * NTHR;
+        int r = ci >> 3, c = ci & 7;
+        *(bf16x8*)(lds + lds_idx(r, c)) = v[i];
+      }
+    }
+  }
+};
+
+template <int AM, int BMODE>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap of the linear block id.
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, loc = bid >> 3;
+    int q = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int bz = blockIdx.y;
+
+  const char* Ab = (const char*)p.A;
+  const char* Bb = (const char*)p.B;
+  const void* Abase = (AM == 2) ? (const void*)(Ab + bz * p.sA * 4) : (const void*)(Ab + bz * p.sA * 2);
+  const void* Bbase = (const void*)(Bb + bz * p.sB * 2);
+
+  Loader<AM> la;
+  Loader<BMODE> lb;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
+
+  const int nk = (p.K + BK - 1) / BK;
+  la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, 0, tid);
+  lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, 0, tid);
+  la.store(smem, tid);
+  lb.store(smem + BM * BK, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    bf16* sa = smem + (kt & 1) * (BM + BN) * BK;
+    bf16* sb = sa + BM * BK;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid);
+      lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, (kt + 1) * BK, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ch = kk * 2 + (lane >> 5);
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sa + lds_idx(wm * 64 + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = *(const bf16x8*)(sb + lds_idx(wn * 64 + j * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      bf16* na = smem + ((kt + 1) & 1) * (BM + BN) * BK;
+      la.store(na, tid);
+      lb.store(na + BM * BK, tid);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue.
+  char* Cb = (char*)p.C + bz * p.sC * (p.c_f32 ? 4 : 2);
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = col0 + wn * 64 + j * 32 + (lane & 31);
+    if (n >= p.N) continue;
+    const float bv = p.bias ? p.bias[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = row0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= p.M) continue;
+        int om = m;
+        if (p.row_map) {
+          om = p.row_map[m];
+          if (om < 0) continue;
+        }
+        const long long ci = (long long)om * p.ldc + n;
+        float v = acc[i][j][r] * p.alpha;
+        if (p.beta != 0.0f) v += p.beta * (p.c_f32 ? ((float*)Cb)[ci] : (float)((bf16*)Cb)[ci]);
+        v += bv;
+        if (Pb) {
+          if (p.pre_f32) ((float*)Pb)[ci] = v;
+          else ((bf16*)Pb)[ci] = (bf16)v;
+        }
+        if (p.act == OCTSAM_ACT_RELU) v = fmaxf(v, 0.0f);
+        else if (p.act == OCTSAM_ACT_GELU) v = gelu_erf(v);
+        if (Rb) {
+          const long long ri = (long long)om * p.ldr + n;
+          v += p.r_f32 ? ((const float*)Rb)[ri] : (float)((const bf16*)Rb)[ri];
+        }
+        if (p.c_f32) ((float*)Cb)[ci] = v;
+        else ((bf16*)Cb)[ci] = (bf16)v;
+      }
+    }
+  }
+}
+
+template <int AM, int BMODE>
+int launch(const GemmK& k, int batch, hipStream_t s) {
+  dim3 grid(k.tiles_m * k.tiles_n, batch);
+  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NTHR), 0, s, k);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+// Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
+__global__ void splitk_reduce_kernel(const float* part, float* out, long long n, int splits, float beta) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.0f;
+  for (int j = 0; j < splits; ++j) s += part[j * n + i];
+  out[i] = (beta != 0.0f ? beta * out[i] : 0.0f) + s;
+}
+
+}  // namespace
+
+extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
+  OCTSAM_CHECK_ARG(a != nullptr, "octsam_gemm: null args");
+  OCTSAM_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0 && a->batch > 0, "octsam_gemm: bad sizes M=%d N=%d K=%d batch=%d",
+                   a->M, a->N, a->K, a->batch);
+  OCTSAM_CHECK_ARG(a->A && a->B && a->C, "octsam_gemm: null operand");
+  OCTSAM_CHECK_ARG(a->a_mode >= 0 && a->a_mode <= 4 && a->b_mode >= 0 && a->b_mode <= 2, "octsam_gemm: bad mode");
+  OCTSAM_CHECK_ARG(a->K % 8 == 0, "octsam_gemm: K=%d must be a multiple of 8", a->K);
+  if (a->a_mode == 1) OCTSAM_CHECK_ARG(a->M % 8 == 0 && a->lda % 8 == 0, "octsam_gemm: transposed A needs M%%8==0");
+  if (a->a_mode == 0 || a->a_mode == 4) OCTSAM_CHECK_ARG(a->lda % 8 == 0, "octsam_gemm: lda must be a multiple of 8");
+  if (a->a_mode == 4) OCTSAM_CHECK_ARG(a->A2 && a->a2_rows > 0, "octsam_gemm: a_mode 4 needs A2 and a2_rows");
+  if (a->b_mode == 2) OCTSAM_CHECK_ARG(a->B2 && a->b2_rows > 0, "octsam_gemm: b_mode 2 needs B2 and b2_rows");
+  if (a->b_mode >= 1) OCTSAM_CHECK_ARG(a->N % 8 == 0 && a->ldb % 8 == 0, "octsam_gemm: transposed B needs N%%8==0");
+  if (a->b_mode == 0) OCTSAM_CHECK_ARG(a->ldb % 8 == 0, "octsam_gemm: ldb must be a multiple of 8");
+  if (a->a_mode == 2) OCTSAM_CHECK_ARG(a->K == 768 && a->M % 4096 == 0, "octsam_gemm: patch16 mode needs K=768, M=B*4096");
+  if (a->a_mode == 3)
+    OCTSAM_CHECK_ARG(a->conv_c % 8 == 0 && a->K == 9 * a->conv_c && a->M % 4096 == 0,
+                     "octsam_gemm: conv3x3 mode needs K=9*C, C%%8==0, M=B*4096");
+  GemmK k;
+  k.A2 = a->A2; k.B2 = a->B2; k.a2_rows = a->a2_rows; k.b2_rows = a->b2_rows;
+  k.A = a->A; k.B = a->B; k.C = a->C; k.bias = a->bias; k.R = a->R; k.Cpre = a->C_pre; k.row_map = a->row_map;
+  k.M = a->M; k.N = a->N; k.K = a->K;
+  k.lda = a->lda; k.ldb = a->ldb; k.ldc = a->ldc; k.ldr = a->ldr;
+  k.sA = a->stride_a; k.sB = a->stride_b; k.sC = a->stride_c; k.sR = a->stride_r;
+  k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
+  k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
+  k.tiles_m = (a->M + BM - 1) / BM;
+  k.tiles_n = (a->N + BN - 1) / BN;
+  hipStream_t s = (hipStream_t)stream;
+  const int am = a->a_mode, bm = a->b_mode;
+  if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);
+  if (am == 0 && bm == 1) return launch<0, 1>(k, a->batch, s);
+  if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);
+  if (am == 1 && bm == 1) return launch<1, 1>(k, a->batch, s);
+  if (am == 2 && bm == 0) return launch<2, 0>(k, a->batch, s);
+  if (am == 3 && bm == 0) return launch<3, 0>(k, a->batch, s);
+  if (am == 4 && bm == 0) return launch<4, 0>(k, a->batch, s);
+  if (am == 1 && bm == 2) return launch<1, 5>(k, a->batch, s);
+  octsam::set_error("octsam_gemm: unsupported mode combination a=%d b=%d", am, bm);
+  return 1;
+}
+
+extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
+                                    void* stream) {
+  OCTSAM_CHECK_ARG(partials && out && n > 0 && splits > 0, "octsam_splitk_reduce: bad args");
+  long long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, partials, out,
+                     n, splits, beta);
+  OCTSAM_LAUNCH_CHECK("octsam_splitk_reduce");
+  return 0;
+}

@@ -1,0 +1,119 @@
+"""GEMM parity: octsam_gemm (MFMA bf16, fp32 accumulate) vs a plain PyTorch fp32 reference on the
+same bf16-rounded operands, for every operand mode the model uses."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (128, 128, 64), (4096, 768, 768), (7, 40, 256)])
+@pytest.mark.parametrize("b_mode", [0, 1])
+def test_gemm_nt_nn(cuda, M, N, K, b_mode):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + b_mode)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    Bw = torch.randn(N, K, generator=g).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda)
+    Bop = Bw if b_mode == 0 else Bw.t().contiguous()
+    out = torch.empty(M, N, device=cuda)
+    pre = torch.empty(M, N, device=cuda)
+    kernels.gemm(A, Bop, M=M, N=N, K=K, out=out, b_mode=b_mode, bias=bias, residual=R, act=2, pre_out=pre)
+    ref_pre = A.float() @ Bw.float().t() + bias
+    ref = F.gelu(ref_pre) + R
+    assert _rel(pre, ref_pre) < 1e-5
+    assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("b_mode", [0, 1])
+def test_gemm_transposed_a(cuda, b_mode):
+    from dilabhelmholtzoct_amd import kernels
+    M, N, K = 256, 136, 520
+    g = torch.Generator().manual_seed(3)
+    At = torch.randn(K, M, generator=g).to(cuda, torch.bfloat16)  # A stored [K, M]
+    Bw = torch.randn(N, K, generator=g).to(cuda, torch.bfloat16)
+    Bop = Bw if b_mode == 0 else Bw.t().contiguous()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    kernels.gemm(At, Bop, M=M, N=N, K=K, out=out, a_mode=1, b_mode=b_mode, act=1)
+    ref = torch.relu(At.float().t() @ Bw.float().t())
+    assert _rel(out, ref) < 8e-3
+
+
+def test_gemm_batched_beta_rowmap(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    Bt, M, N, K = 3, 130, 72, 64
+    g = torch.Generator().manual_seed(4)
+    A = torch.randn(Bt, M, K, generator=g).to(cuda, torch.bfloat16)
+    W = torch.randn(Bt, N, K, generator=g).to(cuda, torch.bfloat16)
+    C0 = torch.randn(Bt, M, N, generator=g).to(cuda)
+    out = C0.clone()
+    kernels.gemm(A, W, M=M, N=N, K=K, out=out, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c=M * N,
+                 alpha=0.5, beta=2.0)
+    ref = 0.5 * torch.bmm(A.float(), W.float().transpose(1, 2)) + 2.0 * C0
+    assert _rel(out, ref) < 1e-5
+    # row_map: reverse rows and drop every third
+    rm = torch.arange(M - 1, -1, -1, dtype=torch.int32)
+    rm[::3] = -1
+    rm = rm.to(cuda)
+    out2 = torch.zeros(M, N, device=cuda)
+    kernels.gemm(A[0], W[0], M=M, N=N, K=K, out=out2, row_map=rm)
+    full = A[0].float() @ W[0].float().t()
+    ref2 = torch.zeros(M, N, device=cuda)
+    keep = (rm >= 0).nonzero().flatten()
+    ref2[rm[keep].long()] = full[keep]
+    assert _rel(out2, ref2) < 1e-5
+
+
+def test_gemm_patch16(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(5)
+    px = torch.randn(2, 3, 1024, 1024, generator=g).to(cuda)
+    W = (0.05 * torch.randn(96, 3, 16, 16, generator=g)).to(cuda, torch.bfloat16)
+    out = torch.empty(2 * 4096, 96, device=cuda)
+    kernels.gemm(px, W.reshape(96, 768), M=2 * 4096, N=96, K=768, out=out, a_mode=2)
+    ref = F.conv2d(px.to(torch.bfloat16).float(), W.float(), stride=16).permute(0, 2, 3, 1).reshape(-1, 96)
+    assert _rel(out, ref) < 1e-5
+
+
+def test_gemm_conv3x3(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(6)
+    C, Co = 32, 48
+    x = torch.randn(2, 64, 64, C, generator=g).to(cuda, torch.bfloat16)  # NHWC
+    W = (0.1 * torch.randn(Co, C, 3, 3, generator=g)).to(cuda, torch.bfloat16)
+    Wr = W.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous()  # k = (ky,kx,c)
+    out = torch.empty(2 * 4096, Co, device=cuda)
+    kernels.gemm(x, Wr, M=2 * 4096, N=Co, K=9 * C, out=out, a_mode=3, conv_c=C)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), W.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    assert _rel(out, ref) < 1e-5
+
+
+def test_gemm_broadcast_addends(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(7)
+    P, L, C, N = 3, 256, 64, 40
+    keys = torch.randn(P * L, C, generator=g).to(cuda, torch.bfloat16)
+    pe = torch.randn(L, C, generator=g).to(cuda, torch.bfloat16)
+    W = torch.randn(N, C, generator=g).to(cuda, torch.bfloat16)
+    out = torch.empty(P * L, N, device=cuda)
+    kernels.gemm(keys, W, M=P * L, N=N, K=C, out=out, a_mode=4, A2=pe, a2_rows=L)
+    summed = (keys.float().view(P, L, C) + pe.float()).to(torch.bfloat16).float().view(P * L, C)
+    assert _rel(out, summed @ W.float().t()) < 1e-5
+    # dW = dY^T (keys + pe): A = dY stored [M, N] (transposed mode), B = keys + pe stored [M, C]
+    dY = torch.randn(P * L, N, generator=g).to(cuda, torch.bfloat16)
+    dW = torch.empty(N, C, device=cuda)
+    kernels.gemm(dY, keys, M=N, N=C, K=P * L, out=dW, a_mode=1, b_mode=2, B2=pe, b2_rows=L)
+    assert _rel(dW, dY.float().t() @ summed) < 1e-5
+
+
+def test_splitk_reduce(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    part = torch.randn(5, 1000, device=cuda)
+    out = torch.ones(1000, device=cuda)
+    kernels.splitk_reduce(part, out, 5, beta=1.0)
+    assert torch.allclose(out, part.sum(0) + 1, atol=1e-5)
