@@ -44,6 +44,14 @@ _SIGNATURES = {
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
     "octsam_cubical_ph": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
+    "octsam_layernorm_fwd": (c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
+                                       c_float, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
+                                       c_void_p]),
+    "octsam_layernorm_bwd": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_float,
+                                       c_void_p, c_void_p, c_int32, c_void_p]),
+    "octsam_vit_attention": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                       c_int32, c_void_p]),
 }
 
 _lib = None

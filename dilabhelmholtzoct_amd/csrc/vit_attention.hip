@@ -1,0 +1,387 @@
+// SAM ViT attention with decomposed relative-position bias, fused (flash-style), forward only.
+//
+// Replaces SamVisionAttention / SamVisionSdpaAttention.forward (hf:modeling_sam.py:803-882) together
+// with get_rel_pos / get_decomposed_rel_pos (:729-801). The [B*h, T, T] bias tensor that HF
+// materialises (805 MB per image for a global vit-b layer) is never formed:
+//
+//   s[q,k] = (q/8)·k + rel_h[q, kh] + rel_w[q, kw],   rel_h[q,kh] = q·Rh[qh-kh+S-1], rel_w likewise
+//
+// (rel-pos resize is an identity for SAM: 2*max(q,k)-1 == table length).
+//
+// Layout/mapping (one wave = 32 queries, all MFMAs v_mfma_f32_32x32x16_bf16):
+//   S^T = K · Q^T  : A = K rows from LDS (XOR-swizzled), B = Q^T fragments kept in registers
+//                    -> every lane owns ONE query (col) and 16 keys (rows) per 32x32 tile
+//   O^T = V^T · P^T: A = V^T from LDS (padded rows, ds_read_b64), B = P^T taken straight from the
+//                    S^T accumulator registers (bf16-packed, k order permuted to match)
+//   so softmax statistics, the rel-pos terms and the O rescale are all per-lane (plus one
+//   lane^32 exchange) and nothing crosses lanes through LDS in the main loop.
+// rel_h / rel_w tables for the wave's queries are themselves MFMA products P^T = R · Q^T staged
+// once through LDS.
+//
+// Global layers (S=64, T=4096): 4 waves (128 queries = 2 image rows) per workgroup, 64-key tiles
+// (= one key image row, so rel_h is one scalar per lane per tile and rel_w is a fixed register set),
+// register-staged double-buffered K/V tiles.
+// Windowed layers (S=14, T=196): 7 waves (224 queries) per (window, head), the whole window's K/V
+// (padded to 256 keys, masked) resident in LDS.
+#include "common.h"
+#include "../../include/octsam.h"
+
+namespace {
+
+constexpr float kScale = 0.125f;  // 64^-0.5, exact in bf16
+
+__device__ __forceinline__ int ksw(int r, int c) {  // K image [rows][64] bf16, 16-B chunk swizzle
+  return r * 64 + ((c ^ ((r >> 1) & 7)) << 3);
+}
+
+__device__ __forceinline__ bf16x8 scale8(bf16x8 v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (bf16)((float)v[i] * kScale);
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[base + j];
+  return r;
+}
+
+// Row index (within a 32x32 tile) held in accumulator register r by lane half h.
+__device__ __forceinline__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// P^T = R_ext · Qs^T for the wave's 32 queries; writes 8 * P^T (undo the 1/8 in Qs) to
+// prel[j * 33 + ql] for j in [0, 32*NJT) (rows >= 2S-1 are zero).
+template <int NJT>
+__device__ __forceinline__ void relpos_table(const float* __restrict__ R, int nrows, const bf16x8 (&qf)[4],
+                                             float* prel, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int t = 0; t < NJT; ++t) {
+    f32x16 acc = (f32x16)0.0f;
+    const int j = t * 32 + l32;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 a;
+      if (j < nrows) {
+        const float* rp = R + j * 64 + 16 * s + 8 * h;
+        float4 x0 = *(const float4*)rp, x1 = *(const float4*)(rp + 4);
+        a[0] = (bf16)x0.x; a[1] = (bf16)x0.y; a[2] = (bf16)x0.z; a[3] = (bf16)x0.w;
+        a[4] = (bf16)x1.x; a[5] = (bf16)x1.y; a[6] = (bf16)x1.z; a[7] = (bf16)x1.w;
+      } else {
+        a = (bf16x8)(bf16)0.0f;
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) prel[(t * 32 + acc_row(r, h)) * 33 + l32] = acc[r] * 8.0f;
+  }
+}
+
+// ------------------------------------------------------------------------------------ global
+constexpr int G_NW = 4, G_THR = G_NW * 64;
+constexpr int VT_LD = 68;  // V^T row stride (bf16): 64 keys + 4 pad -> conflict-free ds_read_b64
+
+struct GSmem {
+  bf16 k[2][64 * 64];
+  bf16 vt[2][64 * VT_LD];
+  float prel[G_NW][128 * 33];
+};
+
+__global__ __launch_bounds__(G_THR) void vit_attn_global_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                const float* __restrict__ Rh,
+                                                                const float* __restrict__ Rw, int heads) {
+  constexpr int S = 64, T = 4096;
+  __shared__ __attribute__((aligned(16))) GSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int head = blockIdx.y, seq = blockIdx.z;
+  const int D = heads * 64, ld = 3 * D;
+  const bf16* base = qkv + (long long)seq * T * ld;
+  const int q = blockIdx.x * (G_NW * 32) + wave * 32 + l32;
+  const int qh = q >> 6, qw = q & 63;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h));
+
+  // rel_w: fixed for the whole key loop (key tile = one key image row, kw = row index in tile)
+  float* prel = sm.prel[wave];
+  relpos_table<4>(Rw, 2 * S - 1, qf, prel, lane);
+  __syncthreads();
+  float relw[2][16];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int kw = 32 * t2 + acc_row(r, h);
+      relw[t2][r] = prel[(qw - kw + S - 1) * 33 + l32];
+    }
+  __syncthreads();
+  relpos_table<4>(Rh, 2 * S - 1, qf, prel, lane);  // rel_h read per tile below
+
+  // K/V tile staging: 64 keys x 64 d, 512 16-B chunks of each, 2 per thread.
+  const bf16* kbase = base + D + head * 64;
+  const bf16* vbase = base + 2 * D + head * 64;
+  bf16x8 kreg[2], vreg[2];
+  auto gload = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int ci = tid + i * G_THR;
+      int key = ci >> 3, c = ci & 7;
+      long long off = (long long)(tile * 64 + key) * ld + c * 8;
+      kreg[i] = *(const bf16x8*)(kbase + off);
+      vreg[i] = *(const bf16x8*)(vbase + off);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int ci = tid + i * G_THR;
+      int key = ci >> 3, c = ci & 7;
+      *(bf16x8*)(sm.k[buf] + ksw(key, c)) = kreg[i];
+      bf16* vt = sm.vt[buf];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vt[(c * 8 + e) * VT_LD + key] = vreg[i][e];
+    }
+  };
+
+  f32x16 acc_o[2];
+  acc_o[0] = (f32x16)0.0f;
+  acc_o[1] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  constexpr int NT = T / 64;
+  for (int tile = 0; tile < NT; ++tile) {
+    const int buf = tile & 1;
+    if (tile + 1 < NT) gload(tile + 1);
+    const bf16* sk = sm.k[buf];
+    const bf16* svt = sm.vt[buf];
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      sacc[t2] = (f32x16)0.0f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 a = *(const bf16x8*)(sk + ksw(t2 * 32 + l32, 2 * s + h));
+        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
+      }
+    }
+    // tile = key image row kh
+    const float relh = prel[(qh - tile + S - 1) * 33 + l32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = sacc[t2][r] + relw[t2][r] + relh;
+        sacc[t2][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.0f;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = __expf(sacc[t2][r] - m_new);
+        sacc[t2][r] = p;
+        ls += p;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int td = 0; td < 2; ++td)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc_o[td][r] *= alpha;
+    // O^T += V^T · P^T over the 64 keys (4 k-steps of 16)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int td = 0; td < 2; ++td) {
+        const bf16* row = svt + (td * 32 + l32) * VT_LD + 16 * ks + 4 * h;
+        bf16x4 lo = *(const bf16x4*)row;
+        bf16x4 hi = *(const bf16x4*)(row + 8);
+        bf16x8 vf;
+        vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+        vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
+        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[td], 0, 0, 0);
+      }
+    }
+    if (tile + 1 < NT) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  bf16* orow = out + ((long long)seq * T + q) * D + head * 64;
+#pragma unroll
+  for (int td = 0; td < 2; ++td)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * g + e] * inv);
+      *(bf16x4*)(orow + td * 32 + 8 * g + 4 * h) = o;
+    }
+}
+
+// ------------------------------------------------------------------------------------ window
+constexpr int W_NW = 7, W_THR = W_NW * 64;
+constexpr int W_KEYS = 256;
+constexpr int WVT_LD = W_KEYS + 4;
+
+struct WSmem {
+  bf16 k[W_KEYS * 64];
+  bf16 vt[64 * WVT_LD];
+  float prel[W_NW][2][32 * 33];
+};
+
+__global__ __launch_bounds__(W_THR) void vit_attn_window_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                                const float* __restrict__ Rh,
+                                                                const float* __restrict__ Rw, int heads) {
+  constexpr int S = 14, T = 196;
+  __shared__ __attribute__((aligned(16))) WSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int head = blockIdx.y, win = blockIdx.x;
+  const int D = heads * 64, ld = 3 * D;
+  const bf16* base = qkv + (long long)win * T * ld;
+
+  // stage the whole window's K (row-major, swizzled) and V^T; keys >= 196 zero
+  for (int ci = tid; ci < W_KEYS * 8; ci += W_THR) {
+    int key = ci >> 3, c = ci & 7;
+    bf16x8 kv = (bf16x8)(bf16)0.0f, vv = (bf16x8)(bf16)0.0f;
+    if (key < T) {
+      kv = *(const bf16x8*)(base + (long long)key * ld + D + head * 64 + c * 8);
+      vv = *(const bf16x8*)(base + (long long)key * ld + 2 * D + head * 64 + c * 8);
+    }
+    *(bf16x8*)(sm.k + ksw(key, c)) = kv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm.vt[(c * 8 + e) * WVT_LD + key] = vv[e];
+  }
+
+  const int q = wave * 32 + l32;
+  const bool qvalid = q < T;
+  const int qh = qvalid ? q / S : 0, qw = qvalid ? q % S : 0;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    qf[s] = qvalid ? scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h))
+                   : (bf16x8)(bf16)0.0f;
+  relpos_table<1>(Rw, 2 * S - 1, qf, sm.prel[wave][0], lane);
+  relpos_table<1>(Rh, 2 * S - 1, qf, sm.prel[wave][1], lane);
+  __syncthreads();
+  float relw[S], relh[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    relw[i] = sm.prel[wave][0][(qw - i + S - 1) * 33 + l32];
+    relh[i] = sm.prel[wave][1][(qh - i + S - 1) * 33 + l32];
+  }
+
+  f32x16 acc_o[2];
+  acc_o[0] = (f32x16)0.0f;
+  acc_o[1] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+#pragma unroll
+  for (int tile = 0; tile < W_KEYS / 64; ++tile) {
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      sacc[t2] = (f32x16)0.0f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 a = *(const bf16x8*)(sm.k + ksw(tile * 64 + t2 * 32 + l32, 2 * s + h));
+        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        // key index for lane half 0 and 1 (compile-time), selected by h
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int k0 = tile * 64 + t2 * 32 + acc_row(r, 0);
+        const int k1 = k0 + 4;
+        float b0 = (k0 < T) ? relh[(k0 < T ? k0 : 0) / S] + relw[(k0 < T ? k0 : 0) % S] : -INFINITY;
+        float b1 = (k1 < T) ? relh[(k1 < T ? k1 : 0) / S] + relw[(k1 < T ? k1 : 0) % S] : -INFINITY;
+        float v = sacc[t2][r] + (h ? b1 : b0);
+        sacc[t2][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.0f;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = __expf(sacc[t2][r] - m_new);
+        sacc[t2][r] = p;
+        ls += p;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int td = 0; td < 2; ++td)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc_o[td][r] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int td = 0; td < 2; ++td) {
+        const bf16* row = sm.vt + (td * 32 + l32) * WVT_LD + tile * 64 + 16 * ks + 4 * h;
+        bf16x4 lo = *(const bf16x4*)row;
+        bf16x4 hi = *(const bf16x4*)(row + 8);
+        bf16x8 vf;
+        vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+        vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
+        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[td], 0, 0, 0);
+      }
+    }
+  }
+  if (!qvalid) return;
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  bf16* orow = out + ((long long)win * T + q) * D + head * 64;
+#pragma unroll
+  for (int td = 0; td < 2; ++td)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * g + e] * inv);
+      *(bf16x4*)(orow + td * 32 + 8 * g + 4 * h) = o;
+    }
+}
+
+}  // namespace
+
+extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w,
+                                    int32_t nseq, int32_t side, int32_t heads, int32_t head_dim, void* stream) {
+  OCTSAM_CHECK_ARG(qkv && out && rel_pos_h && rel_pos_w && nseq > 0 && heads > 0,
+                   "octsam_vit_attention: bad args");
+  OCTSAM_CHECK_ARG(head_dim == 64, "octsam_vit_attention: head_dim must be 64 (got %d)", head_dim);
+  hipStream_t s = (hipStream_t)stream;
+  if (side == 64) {
+    dim3 grid(4096 / (G_NW * 32), heads, nseq);
+    hipLaunchKernelGGL(vit_attn_global_kernel, grid, dim3(G_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
+                       rel_pos_w, heads);
+  } else if (side == 14) {
+    dim3 grid(nseq, heads, 1);
+    hipLaunchKernelGGL(vit_attn_window_kernel, grid, dim3(W_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
+                       rel_pos_w, heads);
+  } else {
+    octsam::set_error("octsam_vit_attention: side must be 64 (global) or 14 (window), got %d", side);
+    return 1;
+  }
+  OCTSAM_LAUNCH_CHECK("octsam_vit_attention");
+  return 0;
+}

@@ -73,3 +73,48 @@ def cubical_ph(maps: torch.Tensor, max_pairs: int = 1024):
     _lib.call("octsam_cubical_ph", ptr(maps), nmaps, H, W, max_pairs, ptr(pairs0), ptr(pairs1),
               ptr(essential), ptr(counts))
     return pairs0, pairs1, essential, counts
+
+
+def layernorm_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, out: torch.Tensor, *,
+                  rows: int | None = None, src_rows: torch.Tensor | None = None, act: int = 0,
+                  out2_f32: torch.Tensor | None = None, mean: torch.Tensor | None = None,
+                  rstd: torch.Tensor | None = None) -> torch.Tensor:
+    """LayerNorm over the last dim; see octsam_layernorm_fwd."""
+    _require_cuda(x, w, b, out, src_rows, out2_f32, mean, rstd)
+    D = w.numel()
+    if rows is None:
+        rows = out.numel() // D
+    _lib.call("octsam_layernorm_fwd", ptr(x), int(x.dtype == torch.float32), ptr(src_rows), rows, D, ptr(w),
+              ptr(b), eps, ptr(out), int(out.dtype == torch.float32), ptr(out2_f32), act, ptr(mean), ptr(rstd))
+    return out
+
+
+def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, w: torch.Tensor,
+                  b: torch.Tensor, dx: torch.Tensor, *, act: int = 0, beta: float = 0.0, nblocks: int = 512):
+    """Returns (dx, dw, db); dw/db reduced deterministically from per-block partials."""
+    _require_cuda(dy, x, mean, rstd, w, b, dx)
+    D = w.numel()
+    rows = mean.numel()
+    nblocks = max(1, min(nblocks, (rows + 3) // 4))
+    part = torch.empty((2, nblocks, D), device=dy.device, dtype=torch.float32)
+    _lib.call("octsam_layernorm_bwd", ptr(dy), int(dy.dtype == torch.float32), ptr(x),
+              int(x.dtype == torch.float32), ptr(mean), ptr(rstd), ptr(w), ptr(b), act, rows, D, ptr(dx),
+              int(dx.dtype == torch.float32), beta, ptr(part[0]), ptr(part[1]), nblocks)
+    dw = torch.empty(D, device=dy.device, dtype=torch.float32)
+    db = torch.empty(D, device=dy.device, dtype=torch.float32)
+    splitk_reduce(part[0], dw, nblocks)
+    splitk_reduce(part[1], db, nblocks)
+    return dx, dw, db
+
+
+def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor, rel_pos_w: torch.Tensor, *,
+                  nseq: int, side: int, heads: int) -> torch.Tensor:
+    """Fused SAM ViT attention with decomposed rel-pos bias; see octsam_vit_attention."""
+    _require_cuda(qkv, out, rel_pos_h, rel_pos_w)
+    if qkv.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+        raise ValueError("vit_attention expects bf16 qkv/out")
+    if qkv.numel() != nseq * side * side * 3 * heads * 64:
+        raise ValueError("qkv shape does not match nseq/side/heads")
+    _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rel_pos_h.float().contiguous()),
+              ptr(rel_pos_w.float().contiguous()), nseq, side, heads, 64)
+    return out

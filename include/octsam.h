@@ -92,6 +92,32 @@ int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t s
 int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, int32_t W, int32_t max_pairs,
                       int32_t* pairs0, int32_t* pairs1, int32_t* essential, int32_t* counts, void* stream);
 
+/* ---------------------------------------------------------------- LayerNorm
+ * Replaces nn.LayerNorm / SamLayerNorm (channels_first applied per pixel of NHWC data) of
+ * SamVisionLayer (hf:modeling_sam.py:954-972), SamVisionNeck (:975-992), SamTwoWayAttentionBlock
+ * (:306-348), SamTwoWayTransformer (:363, eps 1e-5) and the mask-decoder upscaling (:519-521).
+ * Forward: y[r] = act(LN(x[src_rows ? src_rows[r] : r])) over the last dim D in {64,256,768,1024,1280};
+ * a negative src_rows[r] writes a zero row (window_partition padding, :900-922). y is bf16 or fp32
+ * (y_f32); y2_f32 (optional) receives an fp32 copy; mean/rstd (optional, fp32 [rows]) are saved.
+ * Backward (D in {64,256,768}): dx = beta*dx + dLN; per-block dw/db partials [nblocks, D] are written
+ * to dw_part/db_part (combine with octsam_splitk_reduce). act must match the forward. */
+int octsam_layernorm_fwd(const void* x, int32_t x_f32, const int32_t* src_rows, int64_t rows, int32_t D,
+                         const float* w, const float* b, float eps, void* y, int32_t y_f32, float* y2_f32,
+                         int32_t act, float* mean, float* rstd, void* stream);
+int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t x_f32, const float* mean,
+                         const float* rstd, const float* w, const float* b, int32_t act, int64_t rows, int32_t D,
+                         void* dx, int32_t dx_f32, float beta, float* dw_part, float* db_part, int32_t nblocks,
+                         void* stream);
+
+/* ---------------------------------------------------------------- ViT attention
+ * Replaces SamVisionAttention.forward + get_decomposed_rel_pos (hf:modeling_sam.py:729-882).
+ * qkv: bf16 [nseq, side*side, 3*heads*64] (the qkv Linear output, column = part*D + head*64 + d);
+ * out: bf16 [nseq, side*side, heads*64]; rel_pos_h/w: fp32 [2*side-1, 64].
+ * side = 64 (global layers, nseq = batch) or 14 (windowed layers, nseq = batch * 25 windows).
+ * softmax(q k^T / 8 + rel_h + rel_w) v with fp32 statistics; the T x T bias is never materialised. */
+int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
+                         int32_t side, int32_t heads, int32_t head_dim, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

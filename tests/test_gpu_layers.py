@@ -1,0 +1,88 @@
+"""LayerNorm and ViT-attention kernels vs plain PyTorch fp32 references of the same ops
+(hf:modeling_sam.py:729-882 restated in fp32 on the same bf16-rounded inputs)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("D", [64, 256, 768])
+@pytest.mark.parametrize("act", [0, 2])
+def test_layernorm_fwd_bwd(cuda, D, act):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(D + act)
+    rows = 1000
+    x = torch.randn(rows, D, generator=g).to(cuda) * 3 + 1
+    w = torch.randn(D, generator=g).to(cuda)
+    b = torch.randn(D, generator=g).to(cuda)
+    y = torch.empty(rows, D, device=cuda)
+    mean = torch.empty(rows, device=cuda)
+    rstd = torch.empty(rows, device=cuda)
+    kernels.layernorm_fwd(x, w, b, 1e-6, y, act=act, mean=mean, rstd=rstd)
+    xr = x.clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    ref = F.layer_norm(xr, (D,), wr, br, 1e-6)
+    if act == 2:
+        ref = F.gelu(ref)
+    assert _rel(y, ref) < 1e-5
+    dy = torch.randn(rows, D, generator=g).to(cuda)
+    ref.backward(dy)
+    dx = torch.empty_like(x)
+    _, dw, db = kernels.layernorm_bwd(dy, x, mean, rstd, w, b, dx, act=act)
+    assert _rel(dx, xr.grad) < 1e-4
+    assert _rel(dw, wr.grad) < 1e-4
+    assert _rel(db, br.grad) < 1e-4
+
+
+def test_layernorm_gather_rows(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    x = torch.randn(10, 768, device=cuda)
+    w = torch.ones(768, device=cuda)
+    b = torch.zeros(768, device=cuda)
+    src = torch.tensor([3, -1, 0, 9, -1], dtype=torch.int32, device=cuda)
+    y = torch.empty(5, 768, device=cuda, dtype=torch.bfloat16)
+    kernels.layernorm_fwd(x, w, b, 1e-6, y, src_rows=src)
+    ref = F.layer_norm(x, (768,), eps=1e-6)
+    assert _rel(y[0], ref[3]) < 1e-2 and _rel(y[2], ref[0]) < 1e-2 and _rel(y[3], ref[9]) < 1e-2
+    assert torch.all(y[1] == 0) and torch.all(y[4] == 0)
+
+
+def _ref_attention(qkv, Rh, Rw, nseq, side, heads):
+    """HF SamVisionAttention math (eager path) in fp32."""
+    T = side * side
+    qkv = qkv.float().reshape(nseq, T, 3, heads, 64).permute(2, 0, 3, 1, 4).reshape(3, nseq * heads, T, 64)
+    q, k, v = qkv.unbind(0)
+    attn = (q * 0.125) @ k.transpose(-2, -1)
+    idx = (torch.arange(side)[:, None] - torch.arange(side)[None, :] + side - 1).to(q.device)
+    Rh_ = Rh.float()[idx]  # [side, side, 64]
+    Rw_ = Rw.float()[idx]
+    rq = q.reshape(-1, side, side, 64)
+    rel_h = torch.einsum("bhwc,hkc->bhwk", rq, Rh_)
+    rel_w = torch.einsum("bhwc,wkc->bhwk", rq, Rw_)
+    bias = (rel_h[:, :, :, :, None] + rel_w[:, :, :, None, :]).reshape(-1, T, T)
+    attn = torch.softmax(attn + bias, dim=-1)
+    o = (attn @ v).reshape(nseq, heads, side, side, 64).permute(0, 2, 3, 1, 4).reshape(nseq, T, heads * 64)
+    return o
+
+
+@pytest.mark.parametrize("side,nseq,heads", [(14, 6, 3), (64, 2, 2)])
+def test_vit_attention(cuda, side, nseq, heads):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(side)
+    T = side * side
+    qkv = torch.randn(nseq, T, 3 * heads * 64, generator=g).to(cuda, torch.bfloat16)
+    Rh = (0.3 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
+    Rw = (0.3 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
+    # the kernel computes rel-pos from bf16 tables; feed the reference the same rounding
+    Rh_b, Rw_b = Rh.to(torch.bfloat16).float(), Rw.to(torch.bfloat16).float()
+    out = torch.empty(nseq, T, heads * 64, device=cuda, dtype=torch.bfloat16)
+    kernels.vit_attention(qkv, out, Rh, Rw, nseq=nseq, side=side, heads=heads)
+    ref = _ref_attention(qkv, Rh_b, Rw_b, nseq, side, heads)
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2, err
