@@ -33,6 +33,8 @@ class GemmArgs(ctypes.Structure):
         ("act", c_int32), ("a_mode", c_int32), ("b_mode", c_int32),
         ("c_f32", c_int32), ("r_f32", c_int32), ("pre_f32", c_int32), ("conv_c", c_int32),
         ("a2_rows", c_int32), ("b2_rows", c_int32),
+        ("a_blk", c_int32), ("a_rep", c_int32), ("b_blk", c_int32), ("b_rep", c_int32),
+        ("r_blk", c_int32), ("r_rep", c_int32),
     ]
 
 
@@ -52,6 +54,46 @@ _SIGNATURES = {
                                        c_void_p, c_void_p, c_int32, c_void_p]),
     "octsam_vit_attention": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                        c_int32, c_void_p]),
+    "octsam_axpby": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int64, c_float, c_float, c_void_p,
+                               c_int32, c_void_p, c_int64, c_void_p]),
+    "octsam_colsum": (c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_void_p]),
+    "octsam_prompt_tokens": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
+    "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "octsam_dec_tok_attn_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                          c_void_p]),
+    "octsam_dec_tok_attn_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_dec_t2i_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                     c_void_p, c_void_p, c_void_p]),
+    "octsam_dec_t2i_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                     c_void_p]),
+    "octsam_dec_i2t_fwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                     c_void_p, c_int64, c_void_p]),
+    "octsam_dec_i2t_bwd_partials": (c_int64, [c_int32, c_int32, c_int32]),
+    "octsam_dec_i2t_bwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                     c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
+    "octsam_mask_dot_fwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "octsam_mask_dot_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]),
+    "octsam_postproc_fwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                      c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "octsam_dice_reduce": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "octsam_dicece_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_float, c_float,
+                                    c_void_p, c_void_p, c_int32, c_void_p]),
+    "octsam_loss_finalize": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int64, ctypes.c_double,
+                                       ctypes.c_double, c_void_p, c_void_p]),
+    "octsam_postproc_bwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_topo_down": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                   c_void_p, c_void_p, c_void_p]),
+    "octsam_topo_bwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                  c_float, c_void_p, c_void_p]),
+    "octsam_w2_host": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, ctypes.c_double, c_void_p, c_void_p]),
+    "octsam_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
+                              c_float, c_float, c_float, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -42,6 +42,7 @@ struct GemmK {
   const void* A2;
   const void* B2;
   int a2_rows, b2_rows;
+  int a_blk, a_rep, b_blk, b_rep, r_blk, r_rep;
   int M, N, K;
   long long lda, ldb, ldc, ldr;
   long long sA, sB, sC, sR;
@@ -51,6 +52,11 @@ struct GemmK {
   int conv_c;  // channels for conv3x3 mode
   int tiles_m, tiles_n;
 };
+
+// repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
+__device__ __forceinline__ long long remap(int row, int blk, int rep) {
+  return blk > 0 ? (long long)(row / (blk * rep)) * blk + row % blk : (long long)row;
+}
 
 __device__ __forceinline__ int lds_idx(int r, int c) {  // bf16 element index in a [rows][64] image
   return r * BK + ((c ^ ((r >> 1) & 7)) << 3);
@@ -69,7 +75,7 @@ struct Loader {
   bf16x8 v[4];
 
   __device__ __forceinline__ void load(const GemmK& p, const void* base, const void* add, int period,
-                                       long long ld, int rows, int row0, int k0, int tid) {
+                                       long long ld, int rows, int row0, int k0, int tid, int blk, int rep) {
     if constexpr (MODE == 4) {
       const bf16* src = (const bf16*)base;
       const bf16* ad = (const bf16*)add;
@@ -79,7 +85,7 @@ struct Loader {
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
         if (gr < rows && gk < p.K) {
-          bf16x8 x = *(const bf16x8*)(src + (long long)gr * ld + gk);
+          bf16x8 x = *(const bf16x8*)(src + remap(gr, blk, rep) * ld + gk);
           bf16x8 y = *(const bf16x8*)(ad + (long long)(gr % period) * ld + gk);
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
@@ -97,7 +103,7 @@ struct Loader {
         int k = ci >> 4, rc = ci & 15;
         int gr = row0 + rc * 8, gk = k0 + k;
         if (gr < rows && gk < p.K) {
-          bf16x8 x = *(const bf16x8*)(src + (long long)gk * ld + gr);
+          bf16x8 x = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
           bf16x8 y = *(const bf16x8*)(ad + (long long)(gk % period) * ld + gr);
 #pragma unroll
           for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
@@ -114,7 +120,7 @@ struct Loader {
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
         if (gr < rows && gk < p.K)
-          v[i] = *(const bf16x8*)(src + (long long)gr * ld + gk);
+          v[i] = *(const bf16x8*)(src + remap(gr, blk, rep) * ld + gk);
         else
           v[i] = (bf16x8)(bf16)0.0f;
       }
@@ -126,7 +132,7 @@ struct Loader {
         int k = ci >> 4, rc = ci & 15;
         int gr = row0 + rc * 8, gk = k0 + k;
         if (gr < rows && gk < p.K)
-          v[i] = *(const bf16x8*)(src + (long long)gk * ld + gr);
+          v[i] = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
         else
           v[i] = (bf16x8)(bf16)0.0f;
       }
@@ -225,8 +231,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
 
   const int nk = (p.K + BK - 1) / BK;
-  la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, 0, tid);
-  lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, 0, tid);
+  la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, 0, tid, p.a_blk, p.a_rep);
+  lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, 0, tid, p.b_blk, p.b_rep);
   la.store(smem, tid);
   lb.store(smem + BM * BK, tid);
   __syncthreads();
@@ -236,8 +242,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
     bf16* sb = sa + BM * BK;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid);
-      lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, (kt + 1) * BK, tid);
+      la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid, p.a_blk, p.a_rep);
+      lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, (kt + 1) * BK, tid, p.b_blk, p.b_rep);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
         if (p.act == OCTSAM_ACT_RELU) v = fmaxf(v, 0.0f);
         else if (p.act == OCTSAM_ACT_GELU) v = gelu_erf(v);
         if (Rb) {
-          const long long ri = (long long)om * p.ldr + n;
+          const long long ri = remap(om, p.r_blk, p.r_rep) * p.ldr + n;
           v += p.r_f32 ? ((const float*)Rb)[ri] : (float)((const bf16*)Rb)[ri];
         }
         if (p.c_f32) ((float*)Cb)[ci] = v;
@@ -328,6 +334,8 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   OCTSAM_CHECK_ARG(a->A && a->B && a->C, "octsam_gemm: null operand");
   OCTSAM_CHECK_ARG(a->a_mode >= 0 && a->a_mode <= 4 && a->b_mode >= 0 && a->b_mode <= 2, "octsam_gemm: bad mode");
   OCTSAM_CHECK_ARG(a->K % 8 == 0, "octsam_gemm: K=%d must be a multiple of 8", a->K);
+  OCTSAM_CHECK_ARG(a->a_blk == 0 || a->a_mode == 0 || a->a_mode == 4, "octsam_gemm: a_blk needs a_mode 0/4");
+  OCTSAM_CHECK_ARG(a->b_blk == 0 || a->b_mode >= 1, "octsam_gemm: b_blk needs b_mode 1/2");
   if (a->a_mode == 1) OCTSAM_CHECK_ARG(a->M % 8 == 0 && a->lda % 8 == 0, "octsam_gemm: transposed A needs M%%8==0");
   if (a->a_mode == 0 || a->a_mode == 4) OCTSAM_CHECK_ARG(a->lda % 8 == 0, "octsam_gemm: lda must be a multiple of 8");
   if (a->a_mode == 4) OCTSAM_CHECK_ARG(a->A2 && a->a2_rows > 0, "octsam_gemm: a_mode 4 needs A2 and a2_rows");
@@ -340,6 +348,9 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
                      "octsam_gemm: conv3x3 mode needs K=9*C, C%%8==0, M=B*4096");
   GemmK k;
   k.A2 = a->A2; k.B2 = a->B2; k.a2_rows = a->a2_rows; k.b2_rows = a->b2_rows;
+  k.a_blk = a->a_blk; k.a_rep = a->a_rep > 0 ? a->a_rep : 1;
+  k.b_blk = a->b_blk; k.b_rep = a->b_rep > 0 ? a->b_rep : 1;
+  k.r_blk = a->r_blk; k.r_rep = a->r_rep > 0 ? a->r_rep : 1;
   k.A = a->A; k.B = a->B; k.C = a->C; k.bias = a->bias; k.R = a->R; k.Cpre = a->C_pre; k.row_map = a->row_map;
   k.M = a->M; k.N = a->N; k.K = a->K;
   k.lda = a->lda; k.ldb = a->ldb; k.ldc = a->ldc; k.ldr = a->ldr;

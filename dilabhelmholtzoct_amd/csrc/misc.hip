@@ -1,0 +1,141 @@
+// Small element-wise / reduction / embedding kernels of the step.
+//   octsam_axpby        out = alpha*a + beta*b[i % b_period]   (residual adds, dense-prompt broadcast
+//                       image_embeddings + dense_prompt_embeddings, hf:modeling_sam.py:499)
+//   octsam_colsum       per-block column partials of a [rows, cols] matrix (bias gradients)
+//   octsam_prompt_tokens SamPromptEncoder._embed_boxes/_embed_points + token concat of SamMaskDecoder
+//                       (hf:modeling_sam.py:613-656, :489-496)
+//   octsam_image_pe     SamModel.get_image_wide_positional_embeddings (hf:modeling_sam.py:1128-1139),
+//                       written [64*64, 256] channels-last
+#include "common.h"
+#include "../../include/octsam.h"
+
+namespace {
+
+__global__ void axpby_kernel(const void* __restrict__ a, int a_f32, const void* __restrict__ b, int b_f32,
+                             long long b_period, float alpha, float beta, void* __restrict__ out, int out_f32,
+                             float* __restrict__ out2, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float va = a ? (a_f32 ? ((const float*)a)[i] : (float)((const bf16*)a)[i]) : 0.0f;
+  float vb = 0.0f;
+  if (b) {
+    long long j = b_period > 0 ? i % b_period : i;
+    vb = b_f32 ? ((const float*)b)[j] : (float)((const bf16*)b)[j];
+  }
+  float v = alpha * va + beta * vb;
+  if (out_f32) ((float*)out)[i] = v;
+  else ((bf16*)out)[i] = (bf16)v;
+  if (out2) out2[i] = v;
+}
+
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, int x_f32, long long rows, int cols,
+                                                     float* __restrict__ part) {
+  // block b sums rows b, b+nb, ... for columns c = tid, tid+256, ...
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    float s = 0.0f;
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x)
+      s += x_f32 ? ((const float*)x)[r * cols + c] : (float)((const bf16*)x)[r * cols + c];
+    part[(long long)blockIdx.x * cols + c] = s;
+  }
+}
+
+__device__ __forceinline__ void pe256(float cx, float cy, const float* __restrict__ G, float* __restrict__ out, int t) {
+  // coordinates in [0,1]: 2c-1, @ G [2,128], * 2pi, [sin, cos]
+  float x = 2.0f * cx - 1.0f, y = 2.0f * cy - 1.0f;
+  for (int j = t; j < 128; j += 64) {
+    float v = x * G[j] + y * G[128 + j];
+    v = 6.283185307179586f * v;
+    out[j] = sinf(v);
+    out[128 + j] = cosf(v);
+  }
+}
+
+// One wave per prompt. tokens: [P, 5 + nsparse, 256] fp32.
+__global__ void prompt_tokens_kernel(const float* __restrict__ boxes, const float* __restrict__ points,
+                                     const int* __restrict__ labels, int P, int npts, const float* __restrict__ G,
+                                     const float* __restrict__ point_embed, const float* __restrict__ not_a_point,
+                                     const float* __restrict__ out_tokens, float input_size, float* __restrict__ tokens) {
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int nsparse = (points ? (boxes ? npts : npts + 1) : 0) + (boxes ? 2 : 0);
+  const int ntok = 5 + nsparse;
+  float* tok = tokens + (long long)p * ntok * 256;
+  for (int i = t; i < 5 * 256; i += 64) tok[i] = out_tokens[i];
+  int slot = 5;
+  if (points) {
+    for (int k = 0; k < npts; ++k, ++slot) {
+      float* o = tok + slot * 256;
+      int lab = labels ? labels[p * npts + k] : 1;
+      float px = points[(p * npts + k) * 2 + 0] + 0.5f, py = points[(p * npts + k) * 2 + 1] + 0.5f;
+      pe256(px / input_size, py / input_size, G, o, t);
+      __syncthreads();
+      for (int j = t; j < 256; j += 64) {
+        float v = o[j];
+        if (lab == -1) v = not_a_point[j];
+        if (lab == -10) v = 0.0f;
+        if (lab == 0) v += point_embed[0 * 256 + j];
+        if (lab == 1) v += point_embed[1 * 256 + j];
+        o[j] = v;
+      }
+    }
+    if (!boxes) {  // pad point (0,0) with label -1 -> not_a_point_embed
+      float* o = tok + slot * 256;
+      for (int j = t; j < 256; j += 64) o[j] = not_a_point[j];
+      ++slot;
+    }
+  }
+  if (boxes) {
+    const float* bx = boxes + p * 4;
+    for (int c = 0; c < 2; ++c, ++slot) {
+      float* o = tok + slot * 256;
+      pe256((bx[2 * c] + 0.5f) / input_size, (bx[2 * c + 1] + 0.5f) / input_size, G, o, t);
+      __syncthreads();
+      for (int j = t; j < 256; j += 64) o[j] += point_embed[(2 + c) * 256 + j];
+    }
+  }
+}
+
+__global__ void image_pe_kernel(const float* __restrict__ G, int size, float* __restrict__ out) {
+  const int pix = blockIdx.x, t = threadIdx.x;
+  const int y = pix / size, x = pix % size;
+  pe256(((float)x + 0.5f) / size, ((float)y + 0.5f) / size, G, out + (long long)pix * 256, t);
+}
+
+}  // namespace
+
+extern "C" int octsam_axpby(const void* a, int32_t a_f32, const void* b, int32_t b_f32, int64_t b_period, float alpha,
+                            float beta, void* out, int32_t out_f32, float* out2_f32, int64_t n, void* stream) {
+  OCTSAM_CHECK_ARG(out && n > 0, "octsam_axpby: bad args");
+  unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(axpby_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, a_f32, b, b_f32, b_period, alpha,
+                     beta, out, out_f32, out2_f32, n);
+  OCTSAM_LAUNCH_CHECK("octsam_axpby");
+  return 0;
+}
+
+extern "C" int octsam_colsum(const void* x, int32_t x_f32, int64_t rows, int32_t cols, float* part, int32_t nblocks,
+                             void* stream) {
+  OCTSAM_CHECK_ARG(x && part && rows > 0 && cols > 0 && nblocks > 0, "octsam_colsum: bad args");
+  hipLaunchKernelGGL(colsum_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, x_f32, rows, cols, part);
+  OCTSAM_LAUNCH_CHECK("octsam_colsum");
+  return 0;
+}
+
+extern "C" int octsam_prompt_tokens(const float* boxes, const float* points, const int32_t* labels, int32_t P,
+                                    int32_t points_per_prompt, const float* pos_gauss, const float* point_embed,
+                                    const float* not_a_point, const float* out_tokens, float input_size,
+                                    float* tokens, void* stream) {
+  OCTSAM_CHECK_ARG(P > 0 && pos_gauss && point_embed && not_a_point && out_tokens && tokens,
+                   "octsam_prompt_tokens: bad args");
+  OCTSAM_CHECK_ARG(boxes || points, "octsam_prompt_tokens: need boxes or points");
+  hipLaunchKernelGGL(prompt_tokens_kernel, dim3(P), dim3(64), 0, (hipStream_t)stream, boxes, points, labels, P,
+                     points_per_prompt, pos_gauss, point_embed, not_a_point, out_tokens, input_size, tokens);
+  OCTSAM_LAUNCH_CHECK("octsam_prompt_tokens");
+  return 0;
+}
+
+extern "C" int octsam_image_pe(const float* pos_gauss, int32_t size, float* out, void* stream) {
+  OCTSAM_CHECK_ARG(pos_gauss && out && size > 0, "octsam_image_pe: bad args");
+  hipLaunchKernelGGL(image_pe_kernel, dim3(size * size), dim3(64), 0, (hipStream_t)stream, pos_gauss, size, out);
+  OCTSAM_LAUNCH_CHECK("octsam_image_pe");
+  return 0;
+}

@@ -1,0 +1,111 @@
+// Host-side exact q-Wasserstein distance between two persistence diagrams (L-inf ground metric,
+// diagonal augmentation), with the gradient of the transport cost w.r.t. the first diagram.
+//
+// Replaces torch_topological.nn.WassersteinDistance(q) -> POT ot.emd2 (ref:octsam/models/
+// topological_loss.py:78-82), which the reference also runs on the host in float64. The EMD with
+// weights a = (1,..,1,m), b = (1,..,1,n) over the (n+1)x(m+1) cost matrix is solved as the
+// equivalent (n+m)x(n+m) linear assignment (integral optimal vertex) with the shortest-augmenting-
+// path Hungarian method. Cost entries are formed in fp32 exactly as torch does (cdist p=inf and
+// vector_norm to the diagonal, then **q) before the float64 solve.
+// Gradient semantics follow torch autograd: cdist p=inf gives sign(diff) to every coordinate that
+// attains the max; the diagonal distance |d-b|/2 gives (-1/2, +1/2)*sign(d-b).
+// Optimal plans are not unique under ties; POT's network simplex may pick a different optimal plan
+// (same cost, different subgradient): gradient parity under such ties is unpinned.
+#include <cmath>
+#include <cstdint>
+#include <limits>
+#include <vector>
+
+#include "../../include/octsam.h"
+
+namespace {
+
+// e-maxx Hungarian, 1-based, minimisation; returns assignment row -> col (0-based)
+std::vector<int> hungarian(const std::vector<double>& a, int N) {
+  const double INF = std::numeric_limits<double>::infinity();
+  std::vector<double> u(N + 1, 0.0), v(N + 1, 0.0), minv(N + 1);
+  std::vector<int> p(N + 1, 0), way(N + 1, 0);
+  std::vector<char> used(N + 1);
+  for (int i = 1; i <= N; ++i) {
+    p[0] = i;
+    int j0 = 0;
+    std::fill(minv.begin(), minv.end(), INF);
+    std::fill(used.begin(), used.end(), 0);
+    do {
+      used[j0] = 1;
+      int i0 = p[j0], j1 = 0;
+      double delta = INF;
+      for (int j = 1; j <= N; ++j)
+        if (!used[j]) {
+          double cur = a[(i0 - 1) * N + (j - 1)] - u[i0] - v[j];
+          if (cur < minv[j]) { minv[j] = cur; way[j] = j0; }
+          if (minv[j] < delta) { delta = minv[j]; j1 = j; }
+        }
+      for (int j = 0; j <= N; ++j)
+        if (used[j]) { u[p[j]] += delta; v[j] -= delta; }
+        else minv[j] -= delta;
+      j0 = j1;
+    } while (p[j0] != 0);
+    do {
+      int j1 = way[j0];
+      p[j0] = p[j1];
+      j0 = j1;
+    } while (j0);
+  }
+  std::vector<int> row2col(N, -1);
+  for (int j = 1; j <= N; ++j)
+    if (p[j] > 0) row2col[p[j] - 1] = j - 1;
+  return row2col;
+}
+
+inline float linf(float a0, float a1, float b0, float b1) { return std::fmax(std::fabs(a0 - b0), std::fabs(a1 - b1)); }
+inline float diag_dist(float b, float d) {
+  float h = 0.5f * (b + d);
+  return std::fmax(std::fabs(b - h), std::fabs(d - h));
+}
+inline float powq(float x, double q) { return q == 2.0 ? x * x : (float)std::pow((double)x, q); }
+inline float sgn(float x) { return (x > 0.0f) - (x < 0.0f); }
+
+}  // namespace
+
+extern "C" int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_host, int32_t m, double q,
+                              double* cost_host, float* grad_d1_host) {
+  if (n < 0 || m < 0 || !cost_host || (n > 0 && (!d1_host || !grad_d1_host)) || (m > 0 && !d2_host)) return 1;
+  for (int i = 0; i < 2 * n; ++i) grad_d1_host[i] = 0.0f;
+  const int N = n + m;
+  if (N == 0) { *cost_host = 0.0; return 0; }
+  std::vector<double> C((size_t)N * N, 0.0);
+  std::vector<float> dg1(n), dg2(m);
+  for (int i = 0; i < n; ++i) dg1[i] = powq(diag_dist(d1_host[2 * i], d1_host[2 * i + 1]), q);
+  for (int j = 0; j < m; ++j) dg2[j] = powq(diag_dist(d2_host[2 * j], d2_host[2 * j + 1]), q);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      double c;
+      if (i < n && j < m) c = powq(linf(d1_host[2 * i], d1_host[2 * i + 1], d2_host[2 * j], d2_host[2 * j + 1]), q);
+      else if (i < n) c = dg1[i];
+      else if (j < m) c = dg2[j];
+      else c = 0.0;
+      C[(size_t)i * N + j] = c;
+    }
+  std::vector<int> asg = hungarian(C, N);
+  double cost = 0.0;
+  for (int i = 0; i < N; ++i) cost += C[(size_t)i * N + asg[i]];
+  *cost_host = cost;
+  for (int i = 0; i < n; ++i) {
+    const int j = asg[i];
+    const float b = d1_host[2 * i], d = d1_host[2 * i + 1];
+    if (j < m) {
+      const float e0 = b - d2_host[2 * j], e1 = d - d2_host[2 * j + 1];
+      const float M = std::fmax(std::fabs(e0), std::fabs(e1));
+      const float coef = (float)(q * std::pow((double)M, q - 1.0));
+      grad_d1_host[2 * i] = coef * (std::fabs(e0) == M ? sgn(e0) : 0.0f);
+      grad_d1_host[2 * i + 1] = coef * (std::fabs(e1) == M ? sgn(e1) : 0.0f);
+    } else {
+      const float M = diag_dist(b, d);
+      const float coef = (float)(q * std::pow((double)M, q - 1.0));
+      grad_d1_host[2 * i] = coef * 0.5f * sgn(b - d);
+      grad_d1_host[2 * i + 1] = coef * 0.5f * sgn(d - b);
+    }
+  }
+  return 0;
+}

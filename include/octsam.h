@@ -48,6 +48,9 @@ const char* octsam_last_error(void);
  * epilogue: v = alpha*acc + beta*C_old + bias[n]; C_pre = v (optional); v = act(v);
  *           v += R[m*ldr+n] (optional); C = v.  row_map (optional, int32 [M]) redirects output
  *           row m to row_map[m] (skipped when < 0) for C, C_pre and R.
+ * repeat_interleave remaps (hf:modeling_sam.py:499-501): when *_blk > 0 the stored row of logical
+ * row i is (i / (blk*rep)) * blk + i % blk for A rows (a_mode 0/4), B k-rows (b_mode 1/2) and
+ * R rows, so per-image tensors are consumed per prompt without being replicated.
  */
 typedef struct octsam_gemm_args {
   const void* A;
@@ -68,6 +71,7 @@ typedef struct octsam_gemm_args {
   int32_t c_f32, r_f32, pre_f32; /* 1 = fp32 storage, 0 = bf16 */
   int32_t conv_c;
   int32_t a2_rows, b2_rows;
+  int32_t a_blk, a_rep, b_blk, b_rep, r_blk, r_rep;
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);
@@ -117,6 +121,110 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
  * softmax(q k^T / 8 + rel_h + rel_w) v with fp32 statistics; the T x T bias is never materialised. */
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
                          int32_t side, int32_t heads, int32_t head_dim, void* stream);
+
+/* ---------------------------------------------------------------- element-wise / reductions / prompts */
+/* out[i] = alpha*a[i] + beta*b[b_period ? i % b_period : i]  (a or b may be NULL = 0); out2_f32 optional copy.
+ * e.g. image_embeddings + dense_prompt_embeddings (hf:modeling_sam.py:499, b_period = 256 channels). */
+int octsam_axpby(const void* a, int32_t a_f32, const void* b, int32_t b_f32, int64_t b_period, float alpha, float beta,
+                 void* out, int32_t out_f32, float* out2_f32, int64_t n, void* stream);
+/* per-block column sums of x [rows, cols] into part [nblocks, cols] (bias gradients; combine with
+ * octsam_splitk_reduce). */
+int octsam_colsum(const void* x, int32_t x_f32, int64_t rows, int32_t cols, float* part, int32_t nblocks, void* stream);
+/* SamPromptEncoder._embed_boxes / _embed_points (hf:modeling_sam.py:613-656) + the token concat of
+ * SamMaskDecoder.forward (:489-496): tokens [P, 5 + nsparse, 256] fp32 = [iou, mask x4, sparse...].
+ * boxes fp32 [P,4] (x0,y0,x1,y1 in the 1024 frame) and/or points fp32 [P,npts,2] with int32 labels
+ * [P,npts] (NULL = all 1). nsparse = 2 (boxes), npts+1 (points, pad point added), npts+2 (both). */
+int octsam_prompt_tokens(const float* boxes, const float* points, const int32_t* labels, int32_t P,
+                         int32_t points_per_prompt, const float* pos_gauss, const float* point_embed,
+                         const float* not_a_point, const float* out_tokens, float input_size, float* tokens,
+                         void* stream);
+/* SamModel.get_image_wide_positional_embeddings (hf:modeling_sam.py:1128-1139) as [size*size, 256]. */
+int octsam_image_pe(const float* pos_gauss, int32_t size, float* out, void* stream);
+/* bf16 copy of an fp32 buffer */
+int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------- mask decoder attention cores
+ * SamAttention core softmax(q k^T / sqrt(dh)) v (hf:modeling_sam.py:231-270) for the three shapes of
+ * SamTwoWayTransformer; projections are octsam_gemm. T, Tq, Tk <= 8; L = 4096 image tokens.
+ * tok: q,k,v fp32 [P,T,256] (8 heads x 32) -> out bf16; probs fp32 [P,8,T,T] saved for backward.
+ * t2i: q fp32 [P,Tq,128] (8 heads x 16); k,v bf16 rows of [.., L, ldkv], block p/kv_rep
+ *      (kv_rep = prompts per image when K/V are per image); out bf16 [P,Tq,128]; lse fp32 [P,8,Tq].
+ *      backward writes dq bf16 [P,Tq,128] and per-prompt dk, dv bf16 [P, L, lddkv].
+ * i2t: q bf16 rows of [.., L, ldq], block p/q_rep; k,v fp32 [P,Tk,128]; out bf16 [P, L, ldo].
+ *      backward writes dq bf16 [P, L, lddq] and partials fp32 [L/256, P, 2, Tk, 128] (dk; dv),
+ *      reduce with octsam_splitk_reduce; octsam_dec_i2t_bwd_partials() gives the element count. */
+int octsam_dec_tok_attn_fwd(const float* q, const float* k, const float* v, int32_t P, int32_t T, void* out,
+                            float* probs, void* stream);
+int octsam_dec_tok_attn_bwd(const float* q, const float* k, const float* v, const float* probs, const float* dout,
+                            int32_t P, int32_t T, void* dq, void* dk, void* dv, void* stream);
+int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
+                       int32_t L, void* out, float* lse, void* stream);
+int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
+                       int32_t L, const void* out, const float* dout, const float* lse, void* dq, void* dk, void* dv,
+                       int64_t lddkv, void* stream);
+int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
+                       int32_t L, void* out, int64_t ldo, void* stream);
+int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L);
+int octsam_dec_i2t_bwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
+                       int32_t L, const void* dout, int64_t lddo, void* dq, int64_t lddq, float* partials,
+                       void* stream);
+
+/* ---------------------------------------------------------------- mask head
+ * masks = hyper_in @ upscaled_embedding (hf:modeling_sam.py:523-542). up2 bf16 [P, 65536, 32] in the
+ * blocked order of the two ConvTranspose2d GEMMs (pixel y = 4y1+2dy1+dy2, x = 4x1+2dx1+dx2);
+ * hyper fp32 [P, ntok, 32]; masks fp32 [P, ntok, 256, 256]. Backward: dup2pre = (dmask x hyper) *
+ * gelu'(up2pre) (bf16) and partials fp32 [256, P, ntok, 32] of d hyper. */
+int octsam_mask_dot_fwd(const void* up2, const float* hyper, int32_t P, int32_t ntok, float* masks, void* stream);
+int octsam_mask_dot_bwd(const void* up2, const void* up2pre, const float* hyper, int32_t P, int32_t ntok,
+                        const float* dmask, void* dup2pre, float* partials, void* stream);
+
+/* ---------------------------------------------------------------- post-processing + losses
+ * octsam_postproc_fwd: ref:octsam/models/training_utils.py:57-59 — lowres fp32 [M,S,S] -> bilinear to
+ *   mid x mid (align_corners=False) -> crop [:crop_h,:crop_w] -> bilinear to out_h x out_w, fused,
+ *   torch upsample_bilinear2d index arithmetic. With gt (uint8 [M,out_h,out_w], binary) it also writes
+ *   the Dice partial sums dice_part fp32 [M, nblk, 3] = (sum sigmoid(x)*t, sum t, sum sigmoid(x)).
+ * octsam_dice_reduce: monai DiceLoss(sigmoid=True) per map (smooth 1e-5): dice_map double [M] and the
+ *   gradient coefficients coef fp32 [M,2].
+ * octsam_dicece_bwd: CrossEntropyLoss over the prompt dim N with probability targets + the Dice
+ *   gradient: dmask fp32 [B,N,HW] = w_dice*dDice + w_ce*dCE; ce_part double [nblk].
+ * octsam_loss_finalize: loss double [3] = (dice, ce, w_dice*dice + w_ce*ce).
+ * octsam_postproc_bwd: dlowres = composite^T dout with CSR weight tables (cols: for each low-res
+ *   column the (output column, weight) list; rows: likewise); tmp fp32 [M, out_h, S]. */
+int octsam_postproc_fwd(const float* lowres, int32_t M, int32_t S, int32_t mid, int32_t crop_h, int32_t crop_w,
+                        int32_t out_h, int32_t out_w, float* out, const uint8_t* gt, float* dice_part, int32_t nblk,
+                        void* stream);
+int octsam_dice_reduce(const float* dice_part, int32_t M, int32_t nblk, double* dice_map, float* coef, void* stream);
+int octsam_dicece_bwd(const float* masks, const uint8_t* gt, const float* coef, int32_t B, int32_t N, int64_t HW,
+                      float w_dice, float w_ce, float* dmask, double* ce_part, int32_t nblk, void* stream);
+int octsam_loss_finalize(const double* dice_map, int32_t M, const double* ce_part, int32_t nblk, int32_t B, int64_t HW,
+                         double w_dice, double w_ce, double* loss, void* stream);
+int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int32_t out_h, int32_t out_w, const int32_t* col_ptr,
+                        const int32_t* col_idx, const float* col_w, const int32_t* row_ptr, const int32_t* row_idx,
+                        const float* row_w, float* tmp, float* dlowres, void* stream);
+
+/* ---------------------------------------------------------------- topological loss (dense parts)
+ * ref:octsam/models/topological_loss.py:33-46: pred = interp(sigmoid(masks[map_idx[k]]), out_h x out_w,
+ * bilinear, align_corners=True), gt_out likewise from uint8 gt; octsam_topo_bwd adds
+ * scale * d(interp o sigmoid)^T dpred into dmask. Persistence: octsam_cubical_ph; Wasserstein:
+ * octsam_w2_host. */
+int octsam_topo_down(const float* masks, const uint8_t* gt, const int32_t* map_idx, int32_t K, int32_t in_h,
+                     int32_t in_w, int32_t out_h, int32_t out_w, float* pred, float* gt_out, void* stream);
+int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h, int32_t in_w, int32_t out_h,
+                    int32_t out_w, const float* dpred, float scale, float* dmask, void* stream);
+/* HOST function (all pointers host): exact q-Wasserstein transport cost (before the 1/q power)
+ * between diagrams d1 [n,2] and d2 [m,2] with L-inf ground metric and diagonal augmentation
+ * (torch_topological WassersteinDistance -> POT ot.emd2, ref:octsam/models/topological_loss.py:78-82),
+ * and d cost / d d1 [n,2]. */
+int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_host, int32_t m, double q, double* cost_host,
+                   float* grad_d1_host);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.Adam step over a flat fp32 buffer (ref:octsam/models/training_utils.py:31,68):
+ * step_size = lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t) computed by the caller;
+ * params_bf16 (optional) receives the updated parameters in bf16. */
+int octsam_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
+                float beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
+                void* params_bf16, void* stream);
 
 #ifdef __cplusplus
 }
