@@ -51,7 +51,9 @@ _SIGNATURES = {
                                        c_void_p]),
     "octsam_layernorm_bwd": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_float,
-                                       c_void_p, c_void_p, c_int32, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "octsam_relu_bwd": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p]),
+    "octsam_group_sum": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "octsam_vit_attention": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                        c_int32, c_void_p]),
     "octsam_axpby": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int64, c_float, c_float, c_void_p,

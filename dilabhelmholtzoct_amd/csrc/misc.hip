@@ -39,6 +39,28 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
   }
 }
 
+// dx = dy * (y > 0)  (ReLU backward from the saved ReLU output)
+__global__ void relu_bwd_kernel(const float* __restrict__ dy, const bf16* __restrict__ y, long long ldy, int cols,
+                                bf16* __restrict__ dx, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  long long r = i / cols, c = i % cols;
+  float g = (float)y[r * ldy + c] > 0.0f ? dy[i] : 0.0f;
+  dx[i] = (bf16)g;
+}
+
+// out[g][i] = sum_{j<nper} in[(g*nper + j)*n + i]  (sum over the prompts of one image)
+__global__ void group_sum_kernel(const bf16* __restrict__ in, long long ld_in, int cols, int nper, long long rows_per,
+                                 bf16* __restrict__ out, long long total) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  long long per = rows_per * cols;
+  long long g = e / per, rem = e % per, r = rem / cols, c = rem % cols;
+  float s = 0.0f;
+  for (int j = 0; j < nper; ++j) s += (float)in[((g * nper + j) * rows_per + r) * ld_in + c];
+  out[e] = (bf16)s;
+}
+
 __device__ __forceinline__ void pe256(float cx, float cy, const float* __restrict__ G, float* __restrict__ out, int t) {
   // coordinates in [0,1]: 2c-1, @ G [2,128], * 2pi, [sin, cos]
   float x = 2.0f * cx - 1.0f, y = 2.0f * cy - 1.0f;
@@ -137,5 +159,24 @@ extern "C" int octsam_image_pe(const float* pos_gauss, int32_t size, float* out,
   OCTSAM_CHECK_ARG(pos_gauss && out && size > 0, "octsam_image_pe: bad args");
   hipLaunchKernelGGL(image_pe_kernel, dim3(size * size), dim3(64), 0, (hipStream_t)stream, pos_gauss, size, out);
   OCTSAM_LAUNCH_CHECK("octsam_image_pe");
+  return 0;
+}
+
+extern "C" int octsam_relu_bwd(const float* dy, const void* y, int64_t ldy, int32_t cols, void* dx, int64_t n,
+                               void* stream) {
+  OCTSAM_CHECK_ARG(dy && y && dx && cols > 0 && n > 0 && n % cols == 0, "octsam_relu_bwd: bad args");
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dy,
+                     (const bf16*)y, ldy, cols, (bf16*)dx, n);
+  OCTSAM_LAUNCH_CHECK("octsam_relu_bwd");
+  return 0;
+}
+
+extern "C" int octsam_group_sum(const void* in, int64_t ld_in, int32_t cols, int32_t groups, int32_t nper,
+                                int64_t rows_per, void* out, void* stream) {
+  OCTSAM_CHECK_ARG(in && out && cols > 0 && groups > 0 && nper > 0 && rows_per > 0, "octsam_group_sum: bad args");
+  long long total = (long long)groups * rows_per * cols;
+  hipLaunchKernelGGL(group_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)in, ld_in, cols, nper, rows_per, (bf16*)out, total);
+  OCTSAM_LAUNCH_CHECK("octsam_group_sum");
   return 0;
 }

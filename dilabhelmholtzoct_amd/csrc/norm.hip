@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
                                                      const float* __restrict__ rstd, const float* __restrict__ w,
                                                      const float* __restrict__ b, int act, long long rows,
                                                      void* __restrict__ dx, int dx_f32, float beta,
-                                                     float* __restrict__ dw_part, float* __restrict__ db_part) {
+                                                     bf16* __restrict__ dx2, float* __restrict__ dw_part,
+                                                     float* __restrict__ db_part) {
   constexpr int D = PL * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float dwa[PL], dba[PL];
@@ -126,11 +127,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
       float d = rs * (g[i] - s1 - xh[i] * s2);
       if (dx_f32) {
         float* p = (float*)dx + row * D + c;
-        *p = (beta != 0.0f ? beta * *p : 0.0f) + d;
+        d = (beta != 0.0f ? beta * *p : 0.0f) + d;
+        *p = d;
       } else {
         bf16* p = (bf16*)dx + row * D + c;
-        *p = (bf16)((beta != 0.0f ? beta * (float)*p : 0.0f) + d);
+        d = (beta != 0.0f ? beta * (float)*p : 0.0f) + d;
+        *p = (bf16)d;
       }
+      if (dx2) dx2[row * D + c] = (bf16)d;
     }
   }
   // block-level reduction of dw/db partials over the 4 waves through LDS
@@ -159,9 +163,9 @@ int fwd_launch(const void* x, int x_f32, const int* src_rows, long long rows, co
 template <int PL>
 int bwd_launch(const void* dy, int dy_f32, const void* x, int x_f32, const float* mean, const float* rstd,
                const float* w, const float* b, int act, long long rows, void* dx, int dx_f32, float beta,
-               float* dw_part, float* db_part, int nblocks, hipStream_t s) {
+               bf16* dx2, float* dw_part, float* db_part, int nblocks, hipStream_t s) {
   hipLaunchKernelGGL(ln_bwd_kernel<PL>, dim3(nblocks), dim3(256), 0, s, dy, dy_f32, x, x_f32, mean, rstd, w, b, act,
-                     rows, dx, dx_f32, beta, dw_part, db_part);
+                     rows, dx, dx_f32, beta, dx2, dw_part, db_part);
   OCTSAM_LAUNCH_CHECK("octsam_layernorm_bwd");
   return 0;
 }
@@ -186,15 +190,15 @@ extern "C" int octsam_layernorm_fwd(const void* x, int32_t x_f32, const int32_t*
 
 extern "C" int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t x_f32, const float* mean,
                                     const float* rstd, const float* w, const float* b, int32_t act, int64_t rows,
-                                    int32_t D, void* dx, int32_t dx_f32, float beta, float* dw_part, float* db_part,
-                                    int32_t nblocks, void* stream) {
+                                    int32_t D, void* dx, int32_t dx_f32, float beta, void* dx2_bf16, float* dw_part,
+                                    float* db_part, int32_t nblocks, void* stream) {
   OCTSAM_CHECK_ARG(dy && x && mean && rstd && w && b && dx && dw_part && db_part && rows > 0 && nblocks > 0,
                    "octsam_layernorm_bwd: bad args");
   hipStream_t s = (hipStream_t)stream;
   switch (D) {
-    case 64: return bwd_launch<1>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, dw_part, db_part, nblocks, s);
-    case 256: return bwd_launch<4>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, dw_part, db_part, nblocks, s);
-    case 768: return bwd_launch<12>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, dw_part, db_part, nblocks, s);
+    case 64: return bwd_launch<1>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 256: return bwd_launch<4>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 768: return bwd_launch<12>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
     default: octsam::set_error("octsam_layernorm_bwd: unsupported D=%d", D); return 1;
   }
 }

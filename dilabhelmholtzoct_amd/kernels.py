@@ -92,18 +92,23 @@ def layernorm_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
 
 
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor, w: torch.Tensor,
-                  b: torch.Tensor, dx: torch.Tensor, *, act: int = 0, beta: float = 0.0, nblocks: int = 512):
-    """Returns (dx, dw, db); dw/db reduced deterministically from per-block partials."""
-    _require_cuda(dy, x, mean, rstd, w, b, dx)
+                  b: torch.Tensor, dx: torch.Tensor, *, act: int = 0, beta: float = 0.0, nblocks: int = 512,
+                  dx2_bf16: torch.Tensor | None = None, dw: torch.Tensor | None = None,
+                  db: torch.Tensor | None = None):
+    """Returns (dx, dw, db); dw/db reduced deterministically from per-block partials (written into the
+    given dw/db views when provided)."""
+    _require_cuda(dy, x, mean, rstd, w, b, dx, dx2_bf16)
     D = w.numel()
     rows = mean.numel()
     nblocks = max(1, min(nblocks, (rows + 3) // 4))
     part = torch.empty((2, nblocks, D), device=dy.device, dtype=torch.float32)
     _lib.call("octsam_layernorm_bwd", ptr(dy), int(dy.dtype == torch.float32), ptr(x),
               int(x.dtype == torch.float32), ptr(mean), ptr(rstd), ptr(w), ptr(b), act, rows, D, ptr(dx),
-              int(dx.dtype == torch.float32), beta, ptr(part[0]), ptr(part[1]), nblocks)
-    dw = torch.empty(D, device=dy.device, dtype=torch.float32)
-    db = torch.empty(D, device=dy.device, dtype=torch.float32)
+              int(dx.dtype == torch.float32), beta, ptr(dx2_bf16), ptr(part[0]), ptr(part[1]), nblocks)
+    if dw is None:
+        dw = torch.empty(D, device=dy.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(D, device=dy.device, dtype=torch.float32)
     splitk_reduce(part[0], dw, nblocks)
     splitk_reduce(part[1], db, nblocks)
     return dx, dw, db
@@ -120,3 +125,117 @@ def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor,
     _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rel_pos_h.float().contiguous()),
               ptr(rel_pos_w.float().contiguous()), nseq, side, heads, 64)
     return out
+
+
+def _f32(t):
+    return int(t.dtype == torch.float32)
+
+
+def axpby(a, b, out, *, alpha=1.0, beta=1.0, b_period=0, out2_f32=None, n=None):
+    """out = alpha*a + beta*b (b broadcast with period b_period); a or b may be None."""
+    n = out.numel() if n is None else n
+    _lib.call("octsam_axpby", ptr(a), _f32(a) if a is not None else 0, ptr(b), _f32(b) if b is not None else 0,
+              b_period, alpha, beta, ptr(out), _f32(out), ptr(out2_f32), n)
+    return out
+
+
+def cast_bf16(x, out):
+    _lib.call("octsam_cast_bf16", ptr(x), ptr(out), x.numel())
+    return out
+
+
+def colsum(x, rows, cols, out, *, beta=0.0, nblocks=None):
+    """out[c] = beta*out[c] + sum_r x[r, c] (x contiguous [rows, cols]); deterministic."""
+    if nblocks is None:
+        nblocks = max(1, min(512, rows))
+    part = torch.empty((nblocks, cols), device=x.device, dtype=torch.float32)
+    _lib.call("octsam_colsum", ptr(x), _f32(x), rows, cols, ptr(part), nblocks)
+    splitk_reduce(part, out, nblocks, beta=beta)
+    return out
+
+
+def relu_bwd(dy, y, out, *, ldy, cols):
+    _lib.call("octsam_relu_bwd", ptr(dy), ptr(y), ldy, cols, ptr(out), out.numel())
+    return out
+
+
+def group_sum(x, out, *, ld_in, cols, groups, nper, rows_per):
+    _lib.call("octsam_group_sum", ptr(x), ld_in, cols, groups, nper, rows_per, ptr(out))
+    return out
+
+
+def prompt_tokens(boxes, points, labels, P, npts, G, point_embed, not_a_point, out_tokens, input_size, tokens):
+    _lib.call("octsam_prompt_tokens", ptr(boxes), ptr(points), ptr(labels), P, npts, ptr(G), ptr(point_embed),
+              ptr(not_a_point), ptr(out_tokens), input_size, ptr(tokens))
+    return tokens
+
+
+def image_pe(G, size, out):
+    _lib.call("octsam_image_pe", ptr(G), size, ptr(out))
+    return out
+
+
+def tok_attn_fwd(q, k, v, P, T, out, probs):
+    _lib.call("octsam_dec_tok_attn_fwd", ptr(q), ptr(k), ptr(v), P, T, ptr(out), ptr(probs))
+
+
+def tok_attn_bwd(q, k, v, probs, dout, P, T, dq, dk, dv):
+    _lib.call("octsam_dec_tok_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(probs), ptr(dout), P, T, ptr(dq), ptr(dk), ptr(dv))
+
+
+def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse):
+    _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse))
+
+
+def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
+    _lib.call("octsam_dec_t2i_bwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(dout), ptr(lse),
+              ptr(dq), ptr(dk), ptr(dv), lddkv)
+
+
+def i2t_fwd(q, ldq, q_rep, k, v, P, Tk, L, out, ldo):
+    _lib.call("octsam_dec_i2t_fwd", ptr(q), ldq, q_rep, ptr(k), ptr(v), P, Tk, L, ptr(out), ldo)
+
+
+def i2t_bwd(q, ldq, q_rep, k, v, P, Tk, L, dout, lddo, dq, lddq):
+    """Returns dk, dv fp32 [P, Tk, 128] each."""
+    n = _lib.load().octsam_dec_i2t_bwd_partials(P, Tk, L)
+    nb = (L + 255) // 256
+    part = torch.empty(n, device=k.device, dtype=torch.float32)
+    _lib.call("octsam_dec_i2t_bwd", ptr(q), ldq, q_rep, ptr(k), ptr(v), P, Tk, L, ptr(dout), lddo, ptr(dq), lddq,
+              ptr(part))
+    red = torch.empty(P * 2 * Tk * 128, device=k.device, dtype=torch.float32)
+    splitk_reduce(part.view(nb, -1), red, nb)
+    red = red.view(P, 2, Tk, 128)
+    return red[:, 0], red[:, 1]
+
+
+def mask_dot_fwd(up2, hyper, P, ntok, masks):
+    _lib.call("octsam_mask_dot_fwd", ptr(up2), ptr(hyper), P, ntok, ptr(masks))
+    return masks
+
+
+def mask_dot_bwd(up2, up2pre, hyper, P, ntok, dmask, dup2pre, dhyper):
+    part = torch.empty((256, P * ntok * 32), device=up2.device, dtype=torch.float32)
+    _lib.call("octsam_mask_dot_bwd", ptr(up2), ptr(up2pre), ptr(hyper), P, ntok, ptr(dmask), ptr(dup2pre), ptr(part))
+    splitk_reduce(part, dhyper, 256)
+    return dup2pre, dhyper
+
+
+def adam(params, grads, exp_avg, exp_avg_sq, *, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt,
+         params_bf16=None):
+    _lib.call("octsam_adam", ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), params.numel(), beta1, beta2,
+              eps, weight_decay, step_size, bc2_sqrt, ptr(params_bf16))
+
+
+def w2_host(d1: "np.ndarray", d2: "np.ndarray", q: float = 2.0):
+    """Host exact q-Wasserstein transport cost and d cost / d d1 (see octsam_w2_host)."""
+    import numpy as np
+    d1 = np.ascontiguousarray(d1, dtype=np.float32).reshape(-1, 2)
+    d2 = np.ascontiguousarray(d2, dtype=np.float32).reshape(-1, 2)
+    cost = np.zeros(1, np.float64)
+    grad = np.zeros_like(d1)
+    rc = _lib.load().octsam_w2_host(d1.ctypes.data if len(d1) else None, len(d1),
+                                    d2.ctypes.data if len(d2) else None, len(d2), q, cost.ctypes.data,
+                                    grad.ctypes.data if len(d1) else None)
+    _lib.check(rc, "octsam_w2_host")
+    return float(cost[0]), grad

@@ -1,0 +1,427 @@
+"""Drop-in SamModel for the OCT-SAM training step, computed by liboctsam_hip.so.
+
+Mirrors the transformers ``SamModel`` surface the reference uses (hf:modeling_sam.py:1193-1358;
+ref:octsam/models/training_utils.py:55,273-280): same sub-module names (``vision_encoder``,
+``prompt_encoder``, ``mask_decoder``, ``shared_image_embedding``), same parameter names and shapes
+(state_dict keys interchange with HF checkpoints, 315 keys for vit-b), same forward signature and
+output fields (``pred_masks`` [B,N,k,256,256], ``iou_scores`` [B,N,k]). The nn.Linear / nn.Conv2d /
+nn.LayerNorm children are parameter containers only; every forward/backward FLOP runs in HIP kernels.
+
+Precision: bf16 operands with fp32 accumulation on MFMA, fp32 LayerNorm/softmax statistics, fp32
+residual streams in the encoder, fp32 master weights and Adam state for the mask decoder.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .config import SamConfig, config_for
+from ._lib import ACT_GELU
+
+
+# ----------------------------------------------------------------------------------- modules
+class PositionalEmbedding(nn.Module):
+    """SamPositionalEmbedding (hf:modeling_sam.py:546-566): random-Fourier features."""
+
+    def __init__(self, cfg: SamConfig):
+        super().__init__()
+        self.scale = cfg.vision.scale
+        self.positional_embedding = nn.Parameter(torch.zeros(2, cfg.vision.num_pos_feats))
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.projection = nn.Conv2d(3, cfg.hidden_size, kernel_size=16, stride=16)
+
+
+class VisionAttention(nn.Module):
+    def __init__(self, cfg, window_size):
+        super().__init__()
+        side = window_size if window_size > 0 else cfg.image_size // cfg.patch_size
+        self.window_size = window_size
+        self.num_attention_heads = cfg.num_attention_heads
+        self.qkv = nn.Linear(cfg.hidden_size, 3 * cfg.hidden_size)
+        self.proj = nn.Linear(cfg.hidden_size, cfg.hidden_size)
+        hd = cfg.hidden_size // cfg.num_attention_heads
+        self.rel_pos_h = nn.Parameter(torch.zeros(2 * side - 1, hd))
+        self.rel_pos_w = nn.Parameter(torch.zeros(2 * side - 1, hd))
+
+
+class MLPBlock(nn.Module):
+    def __init__(self, d, mlp):
+        super().__init__()
+        self.lin1 = nn.Linear(d, mlp)
+        self.lin2 = nn.Linear(mlp, d)
+
+
+class VisionLayer(nn.Module):
+    def __init__(self, cfg, window_size):
+        super().__init__()
+        self.layer_norm1 = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
+        self.attn = VisionAttention(cfg, window_size)
+        self.layer_norm2 = nn.LayerNorm(cfg.hidden_size, eps=cfg.layer_norm_eps)
+        self.mlp = MLPBlock(cfg.hidden_size, cfg.mlp_dim)
+        self.window_size = window_size
+
+
+class VisionNeck(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cfg.hidden_size, cfg.output_channels, kernel_size=1, bias=False)
+        self.layer_norm1 = nn.LayerNorm(cfg.output_channels, eps=1e-6)
+        self.conv2 = nn.Conv2d(cfg.output_channels, cfg.output_channels, kernel_size=3, padding=1, bias=False)
+        self.layer_norm2 = nn.LayerNorm(cfg.output_channels, eps=1e-6)
+
+
+class VisionEncoder(nn.Module):
+    """SamVisionEncoder (hf:modeling_sam.py:1019-1072): patch-embed -> L ViT layers -> neck."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.config = cfg
+        self.patch_embed = PatchEmbed(cfg)
+        g = cfg.image_size // cfg.patch_size
+        self.pos_embed = nn.Parameter(torch.zeros(1, g, g, cfg.hidden_size))
+        self.layers = nn.ModuleList([
+            VisionLayer(cfg, 0 if i in cfg.global_attn_indexes else cfg.window_size)
+            for i in range(cfg.num_hidden_layers)])
+        self.neck = VisionNeck(cfg)
+        self._wcache: dict = {}
+        self._maps: dict = {}
+
+    # bf16 operand cache, refreshed whenever a parameter is modified in place or moved
+    def _w(self, key, p: torch.Tensor, fn=None):
+        ent = self._wcache.get(key)
+        tag = (p._version, p.data_ptr(), p.device)
+        if ent is None or ent[0] != tag:
+            t = p.detach()
+            t = fn(t) if fn is not None else t
+            ent = (tag, t.to(torch.bfloat16).contiguous())
+            self._wcache[key] = ent
+        return ent[1]
+
+    def _wf(self, key, p: torch.Tensor, fn=None):  # fp32 contiguous copy (biases, LN, pos-embed)
+        ent = self._wcache.get(key)
+        tag = (p._version, p.data_ptr(), p.device)
+        if ent is None or ent[0] != tag:
+            t = p.detach()
+            t = fn(t) if fn is not None else t
+            ent = (tag, t.float().contiguous())
+            self._wcache[key] = ent
+        return ent[1]
+
+    def _window_map(self, B: int, device) -> torch.Tensor:
+        """windowed row -> image row (b*4096 + y*64 + x) or -1 for padding (window_partition,
+        hf:modeling_sam.py:900-952)."""
+        key = (B, str(device))
+        if key not in self._maps:
+            ws, g = self.config.window_size, self.config.image_size // self.config.patch_size
+            nw = (g + ws - 1) // ws
+            b = torch.arange(B).view(B, 1, 1, 1, 1)
+            wy = torch.arange(nw).view(1, nw, 1, 1, 1)
+            wx = torch.arange(nw).view(1, 1, nw, 1, 1)
+            ty = torch.arange(ws).view(1, 1, 1, ws, 1)
+            tx = torch.arange(ws).view(1, 1, 1, 1, ws)
+            y = wy * ws + ty
+            x = wx * ws + tx
+            idx = b * g * g + y * g + x
+            idx = torch.where((y < g) & (x < g), idx, torch.full_like(idx, -1))
+            self._maps[key] = idx.reshape(-1).to(torch.int32).to(device)
+        return self._maps[key]
+
+    @torch.no_grad()
+    def forward_nhwc(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        """pixel_values fp32 [B,3,1024,1024] -> image embeddings fp32 [B, 4096, 256] (NHWC)."""
+        cfg = self.config
+        if pixel_values.dim() != 4 or pixel_values.shape[1] != 3:
+            raise ValueError("Make sure that the channel dimension of the pixel values match with the one set in "
+                             "the configuration.")
+        if pixel_values.shape[2] != cfg.image_size or pixel_values.shape[3] != cfg.image_size:
+            raise ValueError(f"Input image size ({pixel_values.shape[2]}*{pixel_values.shape[3]}) doesn't match "
+                             f"model ({cfg.image_size}*{cfg.image_size}).")
+        px = pixel_values.float().contiguous()
+        B = px.shape[0]
+        D = cfg.hidden_size
+        g = cfg.image_size // cfg.patch_size
+        L = g * g
+        M = B * L
+        dev = px.device
+        heads = cfg.num_attention_heads
+        pe = self.patch_embed.projection
+        x = torch.empty(M, D, device=dev, dtype=torch.float32)
+        K.gemm(px, self._w("patch.w", pe.weight, lambda t: t.reshape(D, -1)), M=M, N=D, K=3 * 256, out=x,
+               a_mode=2, bias=self._wf("patch.b", pe.bias), residual=self._wf("pos", self.pos_embed,
+                                                                                   lambda t: t.reshape(L, D)),
+               r_remap=(L, B))
+        xn = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+        mlp_h = torch.empty(M, cfg.mlp_dim, device=dev, dtype=torch.bfloat16)
+        wmap = None
+        for li, layer in enumerate(self.layers):
+            at = layer.attn
+            ws = layer.window_size
+            pre = f"l{li}."
+            ln1w, ln1b = self._wf(pre + "ln1w", layer.layer_norm1.weight), self._wf(pre + "ln1b", layer.layer_norm1.bias)
+            if ws > 0:
+                if wmap is None:
+                    wmap = self._window_map(B, dev)
+                Mw = wmap.numel()
+                xw = torch.empty(Mw, D, device=dev, dtype=torch.bfloat16)
+                K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xw, src_rows=wmap)
+                qkv = torch.empty(Mw, 3 * D, device=dev, dtype=torch.bfloat16)
+                K.gemm(xw, self._w(pre + "qkv", at.qkv.weight), M=Mw, N=3 * D, K=D, out=qkv,
+                       bias=self._wf(pre + "qkvb", at.qkv.bias))
+                ao = torch.empty(Mw, D, device=dev, dtype=torch.bfloat16)
+                K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
+                                nseq=Mw // (ws * ws), side=ws, heads=heads)
+                K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=Mw, N=D, K=D, out=x,
+                       bias=self._wf(pre + "projb", at.proj.bias), residual=x, row_map=wmap)
+                del xw, qkv, ao
+            else:
+                K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xn)
+                qkv = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+                K.gemm(xn, self._w(pre + "qkv", at.qkv.weight), M=M, N=3 * D, K=D, out=qkv,
+                       bias=self._wf(pre + "qkvb", at.qkv.bias))
+                ao = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+                K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
+                                nseq=B, side=g, heads=heads)
+                K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=M, N=D, K=D, out=x,
+                       bias=self._wf(pre + "projb", at.proj.bias), residual=x)
+                del qkv, ao
+            K.layernorm_fwd(x, self._wf(pre + "ln2w", layer.layer_norm2.weight),
+                            self._wf(pre + "ln2b", layer.layer_norm2.bias), cfg.layer_norm_eps, xn)
+            K.gemm(xn, self._w(pre + "fc1", layer.mlp.lin1.weight), M=M, N=cfg.mlp_dim, K=D, out=mlp_h,
+                   bias=self._wf(pre + "fc1b", layer.mlp.lin1.bias), act=ACT_GELU)
+            K.gemm(mlp_h, self._w(pre + "fc2", layer.mlp.lin2.weight), M=M, N=D, K=cfg.mlp_dim, out=x,
+                   bias=self._wf(pre + "fc2b", layer.mlp.lin2.bias), residual=x)
+        del mlp_h
+        # neck: conv1x1 -> LN2d -> conv3x3 -> LN2d  (channels-last)
+        K.cast_bf16(x, xn)
+        C = cfg.output_channels
+        nk = self.neck
+        y = torch.empty(M, C, device=dev, dtype=torch.float32)
+        K.gemm(xn, self._w("neck.c1", nk.conv1.weight, lambda t: t.reshape(C, D)), M=M, N=C, K=D, out=y)
+        yb = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+        K.layernorm_fwd(y, self._wf("neck.ln1w", nk.layer_norm1.weight), self._wf("neck.ln1b", nk.layer_norm1.bias),
+                        1e-6, yb)
+        K.gemm(yb, self._w("neck.c2", nk.conv2.weight, lambda t: t.permute(0, 2, 3, 1).reshape(C, 9 * C)), M=M,
+               N=C, K=9 * C, out=y, a_mode=3, conv_c=C)
+        emb = torch.empty(B, L, C, device=dev, dtype=torch.float32)
+        K.layernorm_fwd(y, self._wf("neck.ln2w", nk.layer_norm2.weight), self._wf("neck.ln2b", nk.layer_norm2.bias),
+                        1e-6, emb)
+        return emb
+
+    def forward(self, pixel_values):
+        """HF-layout output: last_hidden_state [B, 256, 64, 64]."""
+        emb = self.forward_nhwc(pixel_values)
+        g = self.config.image_size // self.config.patch_size
+        return emb.view(emb.shape[0], g, g, -1).permute(0, 3, 1, 2)
+
+
+class MaskEmbedding(nn.Module):
+    """SamMaskEmbedding parameters (hf:modeling_sam.py:569-598); mask prompts are not used by the
+    reference (input_masks is never passed) and are rejected by this implementation."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        c = cfg.mask_input_channels
+        self.conv1 = nn.Conv2d(1, c // 4, kernel_size=2, stride=2)
+        self.conv2 = nn.Conv2d(c // 4, c, kernel_size=2, stride=2)
+        self.conv3 = nn.Conv2d(c, cfg.hidden_size, kernel_size=1)
+        self.layer_norm1 = nn.LayerNorm(c // 4, eps=1e-6)
+        self.layer_norm2 = nn.LayerNorm(c, eps=1e-6)
+
+
+class PromptEncoder(nn.Module):
+    """SamPromptEncoder (hf:modeling_sam.py:601-698)."""
+
+    def __init__(self, cfg: SamConfig, shared: PositionalEmbedding):
+        super().__init__()
+        pc = cfg.prompt
+        self.shared_embedding = shared
+        self.mask_embed = MaskEmbedding(pc)
+        self.no_mask_embed = nn.Embedding(1, pc.hidden_size)
+        self.point_embed = nn.ModuleList([nn.Embedding(1, pc.hidden_size) for _ in range(pc.num_point_embeddings)])
+        self.not_a_point_embed = nn.Embedding(1, pc.hidden_size)
+        self.input_image_size = pc.image_size
+
+
+# ----------------------------------------------------------------------------------- output
+@dataclass
+class SamImageSegmentationOutput:
+    iou_scores: torch.Tensor = None
+    pred_masks: torch.Tensor = None
+    vision_hidden_states: tuple = None
+    vision_attentions: tuple = None
+    mask_decoder_attentions: tuple = None
+
+    def __getitem__(self, k):
+        return getattr(self, k) if isinstance(k, str) else (self.iou_scores, self.pred_masks)[k]
+
+
+# ----------------------------------------------------------------------------------- model
+class SamModel(nn.Module):
+    """transformers.SamModel drop-in (training surface of ref:octsam/models/training_utils.py)."""
+
+    def __init__(self, config: SamConfig | str = "facebook/sam-vit-base"):
+        super().__init__()
+        from .decoder import MaskDecoder  # local import: decoder imports model helpers
+        cfg = config_for(config) if isinstance(config, str) else config
+        self.config = cfg
+        self.shared_image_embedding = PositionalEmbedding(cfg)
+        self.vision_encoder = VisionEncoder(cfg.vision)
+        self.prompt_encoder = PromptEncoder(cfg, self.shared_image_embedding)
+        self.mask_decoder = MaskDecoder(cfg.decoder)
+
+    # -- weights ----------------------------------------------------------------------
+    @classmethod
+    def from_pretrained(cls, name_or_path: str, **kw) -> "SamModel":
+        """Build the named architecture. A local ``.pt``/``.safetensors`` state dict (HF key layout) is
+        loaded when ``state_dict_path`` is given; hub download is impossible offline, so otherwise the
+        weights are the deterministic synthetic initialisation (seed ``seed``, default 0)."""
+        import os
+        model = cls(kw.pop("config", None) or config_for(os.path.basename(name_or_path.rstrip("/"))
+                                                          if name_or_path not in _ALL_NAMES else name_or_path))
+        path = kw.pop("state_dict_path", None)
+        if path is None and os.path.isfile(name_or_path):
+            path = name_or_path
+        if path:
+            if path.endswith(".safetensors"):
+                from safetensors.torch import load_file
+                sd = load_file(path)
+            else:
+                sd = torch.load(path, map_location="cpu", weights_only=True)
+            model.load_state_dict(sd)
+        else:
+            model.init_weights(seed=kw.pop("seed", 0))
+        return model
+
+    @torch.no_grad()
+    def init_weights(self, seed: int = 0, std: float | None = None):
+        """HF-style initialisation (SamPreTrainedModel._init_weights) with a fixed CPU generator:
+        Linear/Conv/Embedding ~ N(0, 0.02), biases 0, LayerNorm (1, 0). Departures, so that the
+        synthetic model exercises every path: pos_embed and rel_pos tables ~ N(0, 0.02) instead of
+        zeros, and the random-Fourier matrix ~ N(0, 1) instead of N(0, hidden/2)."""
+        std = self.config.initializer_range if std is None else std
+        gen = torch.Generator().manual_seed(seed)
+        for name, p in sorted(self.named_parameters(), key=lambda kv: kv[0]):
+            if name.endswith("positional_embedding"):
+                val = torch.randn(p.shape, generator=gen)
+            elif ".layer_norm" in name or "upscale_layer_norm" in name:
+                val = torch.ones(p.shape) if name.endswith("weight") else torch.zeros(p.shape)
+            elif name.endswith("bias"):
+                val = torch.zeros(p.shape)
+            else:
+                val = torch.randn(p.shape, generator=gen) * std
+            p.copy_(val.to(p.dtype))
+        self.mask_decoder.sync_bf16()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict, assign=False)
+        self.mask_decoder.sync_bf16()
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        super()._apply(fn, *args, **kwargs)
+        self.mask_decoder.reflatten()
+        return self
+
+    # -- pieces -----------------------------------------------------------------------
+    @torch.no_grad()
+    def get_image_wide_positional_embeddings(self) -> torch.Tensor:
+        """[1, 256, 64, 64] like hf:modeling_sam.py:1128-1139."""
+        pe = self.image_pe()
+        g = self.config.prompt.image_embedding_size
+        return pe.view(g, g, -1).permute(2, 0, 1).unsqueeze(0)
+
+    @torch.no_grad()
+    def image_pe(self) -> torch.Tensor:
+        G = self.shared_image_embedding.positional_embedding.detach().float().contiguous()
+        g = self.config.prompt.image_embedding_size
+        out = torch.empty(g * g, 256, device=G.device, dtype=torch.float32)
+        K.image_pe(G, g, out)
+        return out
+
+    @torch.no_grad()
+    def get_image_embeddings(self, pixel_values):
+        return self.vision_encoder(pixel_values)
+
+    @torch.no_grad()
+    def prompt_tokens(self, input_points=None, input_labels=None, input_boxes=None) -> torch.Tensor:
+        """[iou, mask x4, sparse...] tokens [B, N, T, 256] fp32 (decoder input point_embeddings)."""
+        pe = self.prompt_encoder
+        md = self.mask_decoder
+        if input_boxes is not None:
+            B, N = input_boxes.shape[:2]
+        else:
+            B, N = input_points.shape[:2]
+        P = B * N
+        dev = self.shared_image_embedding.positional_embedding.device
+        boxes = input_boxes.reshape(P, 4).to(dev, torch.float32).contiguous() if input_boxes is not None else None
+        pts = labels = None
+        npts = 0
+        if input_points is not None:
+            npts = input_points.shape[2]
+            pts = input_points.reshape(P, npts, 2).to(dev, torch.float32).contiguous()
+            if input_labels is None:
+                labels = torch.ones(P, npts, dtype=torch.int32, device=dev)
+            else:
+                labels = input_labels.reshape(P, npts).to(dev, torch.int32).contiguous()
+        nsparse = (npts + (0 if boxes is not None else 1) if pts is not None else 0) + (2 if boxes is not None else 0)
+        T = 5 + nsparse
+        tokens = torch.empty(P, T, 256, device=dev, dtype=torch.float32)
+        point_embed = torch.cat([e.weight.detach() for e in pe.point_embed], 0).float().contiguous()
+        K.prompt_tokens(boxes, pts, labels, P, npts, self.shared_image_embedding.positional_embedding.detach().float()
+                        .contiguous(), point_embed, pe.not_a_point_embed.weight.detach().float().contiguous(),
+                        md.output_tokens_f32(), float(pe.input_image_size), tokens)
+        return tokens.view(B, N, T, 256)
+
+    # -- forward ----------------------------------------------------------------------
+    def forward(self, pixel_values=None, input_points=None, input_labels=None, input_boxes=None, input_masks=None,
+                image_embeddings=None, multimask_output: bool = True, attention_similarity=None,
+                target_embedding=None, **kwargs) -> SamImageSegmentationOutput:
+        """SamModel.forward (hf:modeling_sam.py:1193-1358); error messages follow HF."""
+        if pixel_values is None and image_embeddings is None:
+            raise ValueError("Either pixel_values or image_embeddings must be provided.")
+        if pixel_values is not None and image_embeddings is not None:
+            raise ValueError("Only one of pixel_values and image_embeddings can be provided.")
+        if input_points is not None and len(input_points.shape) != 4:
+            raise ValueError("The input_points must be a 4D tensor. Of shape `batch_size`, `point_batch_size`, "
+                             f"`nb_points_per_image`, `2`. got {input_points.shape}.")
+        if input_boxes is not None and len(input_boxes.shape) != 3:
+            raise ValueError(f"The input_points must be a 3D tensor. Of shape `batch_size`, `nb_boxes`, `4`. got "
+                             f"{input_boxes.shape}.")
+        if input_points is not None and input_boxes is not None and input_points.shape[1] != input_boxes.shape[1]:
+            raise ValueError("You should provide as many bounding boxes as input points per box. Got "
+                             f"{input_points.shape[1]} and {input_boxes.shape[1]}.")
+        if input_masks is not None or attention_similarity is not None or target_embedding is not None:
+            raise NotImplementedError("mask prompts / attention_similarity / target_embedding are not on the "
+                                      "reference's training path and are not implemented")
+        if input_points is None and input_boxes is None:
+            raise NotImplementedError("prompt-free decoding is not on the reference's training path")
+        if pixel_values is not None:
+            emb = self.vision_encoder.forward_nhwc(pixel_values)
+        else:
+            B_, C_, H_, W_ = image_embeddings.shape
+            emb = image_embeddings.permute(0, 2, 3, 1).reshape(B_, H_ * W_, C_).float().contiguous()
+        tokens = self.prompt_tokens(input_points, input_labels, input_boxes)
+        B, N = tokens.shape[:2]
+        if emb.shape[0] != B:
+            raise ValueError("The batch size of the image embeddings and the input points must be the same. ")
+        masks, iou = self.mask_decoder.run(emb, self.image_pe(), tokens,
+                                           self.prompt_encoder.no_mask_embed.weight, multimask_output)
+        return SamImageSegmentationOutput(iou_scores=iou, pred_masks=masks)
+
+
+_ALL_NAMES = set()
+
+
+def _names():
+    from .config import PRESETS
+    _ALL_NAMES.update(PRESETS)
+
+
+_names()

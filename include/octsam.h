@@ -103,15 +103,15 @@ int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, int32_t W, in
  * Forward: y[r] = act(LN(x[src_rows ? src_rows[r] : r])) over the last dim D in {64,256,768,1024,1280};
  * a negative src_rows[r] writes a zero row (window_partition padding, :900-922). y is bf16 or fp32
  * (y_f32); y2_f32 (optional) receives an fp32 copy; mean/rstd (optional, fp32 [rows]) are saved.
- * Backward (D in {64,256,768}): dx = beta*dx + dLN; per-block dw/db partials [nblocks, D] are written
+ * Backward (D in {64,256,768}): dx = beta*dx + dLN (dx2_bf16 optional bf16 copy); per-block dw/db partials [nblocks, D] are written
  * to dw_part/db_part (combine with octsam_splitk_reduce). act must match the forward. */
 int octsam_layernorm_fwd(const void* x, int32_t x_f32, const int32_t* src_rows, int64_t rows, int32_t D,
                          const float* w, const float* b, float eps, void* y, int32_t y_f32, float* y2_f32,
                          int32_t act, float* mean, float* rstd, void* stream);
 int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t x_f32, const float* mean,
                          const float* rstd, const float* w, const float* b, int32_t act, int64_t rows, int32_t D,
-                         void* dx, int32_t dx_f32, float beta, float* dw_part, float* db_part, int32_t nblocks,
-                         void* stream);
+                         void* dx, int32_t dx_f32, float beta, void* dx2_bf16, float* dw_part, float* db_part,
+                         int32_t nblocks, void* stream);
 
 /* ---------------------------------------------------------------- ViT attention
  * Replaces SamVisionAttention.forward + get_decomposed_rel_pos (hf:modeling_sam.py:729-882).
@@ -140,6 +140,13 @@ int octsam_prompt_tokens(const float* boxes, const float* points, const int32_t*
                          void* stream);
 /* SamModel.get_image_wide_positional_embeddings (hf:modeling_sam.py:1128-1139) as [size*size, 256]. */
 int octsam_image_pe(const float* pos_gauss, int32_t size, float* out, void* stream);
+/* dx bf16 [n] = dy fp32 [n] * (y > 0), y bf16 rows of stride ldy with `cols` columns (ReLU backward) */
+int octsam_relu_bwd(const float* dy, const void* y, int64_t ldy, int32_t cols, void* dx, int64_t n, void* stream);
+/* out bf16 [groups, rows_per, cols] = sum over nper consecutive blocks of in (bf16 rows of stride ld_in):
+ * sums the per-prompt gradients of a tensor that was shared by the prompts of one image
+ * (the backward of repeat_interleave, hf:modeling_sam.py:499-501). */
+int octsam_group_sum(const void* in, int64_t ld_in, int32_t cols, int32_t groups, int32_t nper, int64_t rows_per,
+                     void* out, void* stream);
 /* bf16 copy of an fp32 buffer */
 int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 
