@@ -333,7 +333,9 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
                    a->M, a->N, a->K, a->batch);
   OCTSAM_CHECK_ARG(a->A && a->B && a->C, "octsam_gemm: null operand");
   OCTSAM_CHECK_ARG(a->a_mode >= 0 && a->a_mode <= 4 && a->b_mode >= 0 && a->b_mode <= 2, "octsam_gemm: bad mode");
-  OCTSAM_CHECK_ARG(a->K % 8 == 0, "octsam_gemm: K=%d must be a multiple of 8", a->K);
+  // K-contiguous operand loads move 8 consecutive k at a time; transposed loads move one k per chunk
+  if (a->a_mode != 1 || a->b_mode == 0)
+    OCTSAM_CHECK_ARG(a->K % 8 == 0, "octsam_gemm: K=%d must be a multiple of 8", a->K);
   OCTSAM_CHECK_ARG(a->a_blk == 0 || a->a_mode == 0 || a->a_mode == 4, "octsam_gemm: a_blk needs a_mode 0/4");
   OCTSAM_CHECK_ARG(a->b_blk == 0 || a->b_mode >= 1, "octsam_gemm: b_blk needs b_mode 1/2");
   if (a->a_mode == 1) OCTSAM_CHECK_ARG(a->M % 8 == 0 && a->lda % 8 == 0, "octsam_gemm: transposed A needs M%%8==0");

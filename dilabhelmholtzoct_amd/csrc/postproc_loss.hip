@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void pp_bwd_cols_kernel(const float* __restric
 // topo forward: pred50[k] = interp_ac(sigmoid(masks[map_idx[k]])), gt50[k] = interp_ac(gt[map_idx[k]])
 __global__ __launch_bounds__(256) void topo_down_kernel(const float* __restrict__ masks, const uint8_t* __restrict__ gt,
                                                         const int* __restrict__ map_idx, int ih, int iw, int oh, int ow,
-                                                        float sh, float sw, float* __restrict__ pred,
+                                                        float sh, float sw, int sig, float* __restrict__ pred,
                                                         float* __restrict__ gto) {
   const int k = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -205,7 +205,10 @@ __global__ __launch_bounds__(256) void topo_down_kernel(const float* __restrict_
   const int i = e / ow, j = e % ow;
   const long long mo = (long long)map_idx[k] * ih * iw;
   Lin a = lin_act(i, ih, sh), b = lin_act(j, iw, sw);
-  auto sg = [&](int r, int c) { return 1.0f / (1.0f + __expf(-masks[mo + (long long)r * iw + c])); };
+  auto sg = [&](int r, int c) {
+    float x = masks[mo + (long long)r * iw + c];
+    return sig ? 1.0f / (1.0f + __expf(-x)) : x;
+  };
   auto gv = [&](int r, int c) { return (float)gt[mo + (long long)r * iw + c]; };
   pred[(long long)k * oh * ow + e] =
       a.l0 * (b.l0 * sg(a.i0, b.i0) + b.l1 * sg(a.i0, b.i1)) + a.l1 * (b.l0 * sg(a.i1, b.i0) + b.l1 * sg(a.i1, b.i1));
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(256) void topo_down_kernel(const float* __restrict_
 
 // topo backward: dmask[map_idx[k]] += d(interp_ac o sigmoid)^T dpred[k]
 __global__ __launch_bounds__(256) void topo_bwd_kernel(const float* __restrict__ masks, const int* __restrict__ map_idx,
-                                                       int ih, int iw, int oh, int ow, float sh, float sw,
+                                                       int ih, int iw, int oh, int ow, float sh, float sw, int sig,
                                                        const float* __restrict__ dpred, float scale,
                                                        float* __restrict__ dmask) {
   const int k = blockIdx.y;
@@ -229,8 +232,12 @@ __global__ __launch_bounds__(256) void topo_bwd_kernel(const float* __restrict__
   Lin a = lin_act(i, ih, sh), b = lin_act(j, iw, sw);
   auto add = [&](int r, int c, float w) {
     long long idx = mo + (long long)r * iw + c;
-    float s = 1.0f / (1.0f + __expf(-masks[idx]));
-    atomicAdd(dmask + idx, g * w * s * (1.0f - s));
+    float d = 1.0f;
+    if (sig) {
+      float s = 1.0f / (1.0f + __expf(-masks[idx]));
+      d = s * (1.0f - s);
+    }
+    atomicAdd(dmask + idx, g * w * d);
   };
   add(a.i0, b.i0, a.l0 * b.l0);
   add(a.i0, b.i1, a.l0 * b.l1);
@@ -301,26 +308,27 @@ extern "C" int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int3
 }
 
 extern "C" int octsam_topo_down(const float* masks, const uint8_t* gt, const int32_t* map_idx, int32_t K, int32_t in_h,
-                                int32_t in_w, int32_t out_h, int32_t out_w, float* pred, float* gt_out, void* stream) {
+                                int32_t in_w, int32_t out_h, int32_t out_w, int32_t apply_sigmoid, float* pred,
+                                float* gt_out, void* stream) {
   OCTSAM_CHECK_ARG(masks && map_idx && pred && K >= 0 && in_h > 1 && in_w > 1 && out_h > 1 && out_w > 1,
                    "octsam_topo_down: bad args");
   OCTSAM_CHECK_ARG(!gt_out || gt, "octsam_topo_down: gt_out needs gt");
   if (K == 0) return 0;
   float sh = (float)(in_h - 1) / (float)(out_h - 1), sw = (float)(in_w - 1) / (float)(out_w - 1);
   hipLaunchKernelGGL(topo_down_kernel, dim3((out_h * out_w + 255) / 256, K), dim3(256), 0, (hipStream_t)stream, masks,
-                     gt, map_idx, in_h, in_w, out_h, out_w, sh, sw, pred, gt_out);
+                     gt, map_idx, in_h, in_w, out_h, out_w, sh, sw, apply_sigmoid, pred, gt_out);
   OCTSAM_LAUNCH_CHECK("octsam_topo_down");
   return 0;
 }
 
 extern "C" int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h, int32_t in_w,
-                               int32_t out_h, int32_t out_w, const float* dpred, float scale, float* dmask,
-                               void* stream) {
+                               int32_t out_h, int32_t out_w, int32_t apply_sigmoid, const float* dpred, float scale,
+                               float* dmask, void* stream) {
   OCTSAM_CHECK_ARG(masks && map_idx && dpred && dmask && K >= 0, "octsam_topo_bwd: bad args");
   if (K == 0) return 0;
   float sh = (float)(in_h - 1) / (float)(out_h - 1), sw = (float)(in_w - 1) / (float)(out_w - 1);
   hipLaunchKernelGGL(topo_bwd_kernel, dim3((out_h * out_w + 255) / 256, K), dim3(256), 0, (hipStream_t)stream, masks,
-                     map_idx, in_h, in_w, out_h, out_w, sh, sw, dpred, scale, dmask);
+                     map_idx, in_h, in_w, out_h, out_w, sh, sw, apply_sigmoid, dpred, scale, dmask);
   OCTSAM_LAUNCH_CHECK("octsam_topo_bwd");
   return 0;
 }

@@ -210,14 +210,15 @@ int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int32_t out_h, 
                         const float* row_w, float* tmp, float* dlowres, void* stream);
 
 /* ---------------------------------------------------------------- topological loss (dense parts)
- * ref:octsam/models/topological_loss.py:33-46: pred = interp(sigmoid(masks[map_idx[k]]), out_h x out_w,
- * bilinear, align_corners=True), gt_out likewise from uint8 gt; octsam_topo_bwd adds
- * scale * d(interp o sigmoid)^T dpred into dmask. Persistence: octsam_cubical_ph; Wasserstein:
- * octsam_w2_host. */
+ * ref:octsam/models/topological_loss.py:33-46: pred = interp(f(masks[map_idx[k]]), out_h x out_w,
+ * bilinear, align_corners=True) with f = sigmoid (training_utils.py:64) when apply_sigmoid, else identity;
+ * gt_out likewise from uint8 gt; octsam_topo_bwd adds scale * d(interp o f)^T dpred into dmask.
+ * Persistence: octsam_cubical_ph; Wasserstein: octsam_w2_host. */
 int octsam_topo_down(const float* masks, const uint8_t* gt, const int32_t* map_idx, int32_t K, int32_t in_h,
-                     int32_t in_w, int32_t out_h, int32_t out_w, float* pred, float* gt_out, void* stream);
+                     int32_t in_w, int32_t out_h, int32_t out_w, int32_t apply_sigmoid, float* pred, float* gt_out,
+                     void* stream);
 int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h, int32_t in_w, int32_t out_h,
-                    int32_t out_w, const float* dpred, float scale, float* dmask, void* stream);
+                    int32_t out_w, int32_t apply_sigmoid, const float* dpred, float scale, float* dmask, void* stream);
 /* HOST function (all pointers host): exact q-Wasserstein transport cost (before the 1/q power)
  * between diagrams d1 [n,2] and d2 [m,2] with L-inf ground metric and diagonal augmentation
  * (torch_topological WassersteinDistance -> POT ot.emd2, ref:octsam/models/topological_loss.py:78-82),

@@ -1,7 +1,10 @@
 """End-to-end parity of the HIP SamModel against transformers' SamModel in fp32 (the reference's own
 model code, hf:modeling_sam.py) on the same weights: encoder output, decoder masks (boxes and points),
 and every mask-decoder parameter gradient. bf16 MFMA path vs fp32 reference: tolerances are stated
-per check (relative Frobenius error)."""
+per check (relative Frobenius error). The token-path gradients of this random-init decoder are badly
+conditioned in bf16 (transformers' own SamModel run in bf16 is 10-40 % off its fp32 gradients), so each
+gradient must be at least as close to fp32 as transformers-in-bf16 is (plus 2 % slack), and within 15 %."""
+import copy
 import pytest
 import torch
 
@@ -21,11 +24,14 @@ def models(cuda):
     ours.init_weights(seed=1)
     hf = HFSam(SamConfig())
     hf.load_state_dict(ours.state_dict())
+    hfb = copy.deepcopy(hf)
     ours = ours.to(cuda)
     hf = hf.to(cuda).float().eval()
-    for n, p in hf.named_parameters():
-        p.requires_grad_(n.startswith("mask_decoder"))
-    return ours, hf
+    hfb = hfb.to(cuda).to(torch.bfloat16).eval()
+    for m in (hf, hfb):
+        for n, p in m.named_parameters():
+            p.requires_grad_(n.startswith("mask_decoder"))
+    return ours, hf, hfb
 
 
 def _inputs(cuda, B=2, N=3, seed=0):
@@ -40,7 +46,7 @@ def _inputs(cuda, B=2, N=3, seed=0):
 
 
 def test_encoder_parity(cuda, models):
-    ours, hf = models
+    ours, hf, _ = models
     px, _, _ = _inputs(cuda)
     with torch.no_grad():
         ref = hf.vision_encoder(px).last_hidden_state
@@ -51,7 +57,7 @@ def test_encoder_parity(cuda, models):
 
 @pytest.mark.parametrize("prompt", ["boxes", "points"])
 def test_decoder_forward_backward(cuda, models, prompt):
-    ours, hf = models
+    ours, hf, hfb = models
     px, boxes, pts = _inputs(cuda, seed=3)
     with torch.no_grad():
         emb = hf.vision_encoder(px).last_hidden_state
@@ -61,26 +67,34 @@ def test_decoder_forward_backward(cuda, models, prompt):
     assert out.pred_masks.shape == out_ref.pred_masks.shape
     assert _rel(out.pred_masks, out_ref.pred_masks) < 3e-2
     assert _rel(out.iou_scores, out_ref.iou_scores) < 3e-2
+    kwb = {k: v.bfloat16() for k, v in kw.items()}
+    out_b = hfb(image_embeddings=emb.bfloat16(), multimask_output=False, **kwb)
     w = torch.randn(out_ref.pred_masks.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
     hf.zero_grad()
+    hfb.zero_grad()
     (out_ref.pred_masks * w).sum().backward()
+    (out_b.pred_masks.float() * w).sum().backward()
     (out.pred_masks * w).sum().backward()
     ours.mask_decoder.bind_param_grads()
     ref_g = {n: p.grad for n, p in hf.mask_decoder.named_parameters()}
+    ref_b = {n: p.grad for n, p in hfb.mask_decoder.named_parameters()}
+    scale = max(g.norm().item() for g in ref_g.values() if g is not None)
     bad = {}
     for n, p in ours.mask_decoder.named_parameters():
         r = ref_g[n]
-        if r is None or r.abs().max() == 0:
-            assert p.grad is None or p.grad.abs().max() == 0, n
+        if r is None or r.norm().item() < 1e-6 * scale:
+            # no gradient in the reference (unused heads, softmax-invariant key biases)
+            assert p.grad is None or p.grad.norm().item() < 1e-4 * scale, n
             continue
         e = _rel(p.grad, r)
-        if e > 5e-2:
-            bad[n] = e
+        eb = _rel(ref_b[n].float(), r)
+        if e > min(0.15, eb + 0.02):
+            bad[n] = (e, eb)
     assert not bad, bad
 
 
 def test_multimask_forward(cuda, models):
-    ours, hf = models
+    ours, hf, _ = models
     px, boxes, _ = _inputs(cuda, B=1, N=2, seed=7)
     with torch.no_grad():
         emb = hf.vision_encoder(px).last_hidden_state
