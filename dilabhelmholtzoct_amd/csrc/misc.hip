@@ -39,6 +39,41 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
   }
 }
 
+// Vectorised column sums: thread = (row lane, 8-column group); 16/32-byte loads; LDS combine.
+template <bool F32>
+__global__ __launch_bounds__(256) void colsum8_kernel(const void* __restrict__ x, long long rows, int cols,
+                                                      float* __restrict__ part) {
+  const int G = cols >> 3;
+  const int lanes = 256 / G;
+  const int g = threadIdx.x % G, lane = threadIdx.x / G;
+  __shared__ float red[2048];
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+  if (lane < lanes) {
+    for (long long r = (long long)blockIdx.x * lanes + lane; r < rows; r += (long long)gridDim.x * lanes) {
+      if (F32) {
+        const float4* p = (const float4*)((const float*)x + r * cols + g * 8);
+        float4 a = p[0], b = p[1];
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      } else {
+        bf16x8 v = *(const bf16x8*)((const bf16*)x + r * cols + g * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+      }
+    }
+  }
+  for (int l = 0; l < lanes; ++l) {
+    if (lane == l) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[g * 8 + e] = (l == 0 ? 0.0f : red[g * 8 + e]) + acc[e];
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < cols; c += 256) part[(long long)blockIdx.x * cols + c] = red[c];
+}
+
 // dx = dy * (y > 0)  (ReLU backward from the saved ReLU output)
 __global__ void relu_bwd_kernel(const float* __restrict__ dy, const bf16* __restrict__ y, long long ldy, int cols,
                                 bf16* __restrict__ dx, long long n) {
@@ -137,7 +172,14 @@ extern "C" int octsam_axpby(const void* a, int32_t a_f32, const void* b, int32_t
 extern "C" int octsam_colsum(const void* x, int32_t x_f32, int64_t rows, int32_t cols, float* part, int32_t nblocks,
                              void* stream) {
   OCTSAM_CHECK_ARG(x && part && rows > 0 && cols > 0 && nblocks > 0, "octsam_colsum: bad args");
-  hipLaunchKernelGGL(colsum_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, x_f32, rows, cols, part);
+  if (cols % 8 == 0 && cols <= 2048) {
+    if (x_f32)
+      hipLaunchKernelGGL(colsum8_kernel<true>, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, rows, cols, part);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<false>, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, rows, cols, part);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, x_f32, rows, cols, part);
+  }
   OCTSAM_LAUNCH_CHECK("octsam_colsum");
   return 0;
 }

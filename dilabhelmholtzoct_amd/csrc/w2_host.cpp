@@ -4,8 +4,8 @@
 // Replaces torch_topological.nn.WassersteinDistance(q) -> POT ot.emd2 (ref:octsam/models/
 // topological_loss.py:78-82), which the reference also runs on the host in float64. The EMD with
 // weights a = (1,..,1,m), b = (1,..,1,n) over the (n+1)x(m+1) cost matrix is solved as the
-// equivalent (n+m)x(n+m) linear assignment (integral optimal vertex) with the shortest-augmenting-
-// path Hungarian method. Cost entries are formed in fp32 exactly as torch does (cdist p=inf and
+// equivalent linear assignment (integral optimal vertex), reduced to a rectangular problem over the
+// smaller diagram (see octsam_w2_host), solved with the shortest-augmenting-path Hungarian method. Cost entries are formed in fp32 exactly as torch does (cdist p=inf and
 // vector_norm to the diagonal, then **q) before the float64 solve.
 // Gradient semantics follow torch autograd: cdist p=inf gives sign(diff) to every coordinate that
 // attains the max; the diagonal distance |d-b|/2 gives (-1/2, +1/2)*sign(d-b).
@@ -20,13 +20,15 @@
 
 namespace {
 
-// e-maxx Hungarian, 1-based, minimisation; returns assignment row -> col (0-based)
-std::vector<int> hungarian(const std::vector<double>& a, int N) {
+// e-maxx Hungarian for a rectangular matrix (n rows <= m cols, row-major with stride m), minimisation;
+// O(n^2 m); returns assignment row -> col (0-based)
+std::vector<int> hungarian(const std::vector<double>& a, int n, int m) {
   const double INF = std::numeric_limits<double>::infinity();
-  std::vector<double> u(N + 1, 0.0), v(N + 1, 0.0), minv(N + 1);
+  const int N = m;
+  std::vector<double> u(n + 1, 0.0), v(N + 1, 0.0), minv(N + 1);
   std::vector<int> p(N + 1, 0), way(N + 1, 0);
   std::vector<char> used(N + 1);
-  for (int i = 1; i <= N; ++i) {
+  for (int i = 1; i <= n; ++i) {
     p[0] = i;
     int j0 = 0;
     std::fill(minv.begin(), minv.end(), INF);
@@ -52,7 +54,7 @@ std::vector<int> hungarian(const std::vector<double>& a, int N) {
       j0 = j1;
     } while (j0);
   }
-  std::vector<int> row2col(N, -1);
+  std::vector<int> row2col(n, -1);
   for (int j = 1; j <= N; ++j)
     if (p[j] > 0) row2col[p[j] - 1] = j - 1;
   return row2col;
@@ -72,29 +74,50 @@ extern "C" int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_h
                               double* cost_host, float* grad_d1_host) {
   if (n < 0 || m < 0 || !cost_host || (n > 0 && (!d1_host || !grad_d1_host)) || (m > 0 && !d2_host)) return 1;
   for (int i = 0; i < 2 * n; ++i) grad_d1_host[i] = 0.0f;
-  const int N = n + m;
-  if (N == 0) { *cost_host = 0.0; return 0; }
-  std::vector<double> C((size_t)N * N, 0.0);
   std::vector<float> dg1(n), dg2(m);
   for (int i = 0; i < n; ++i) dg1[i] = powq(diag_dist(d1_host[2 * i], d1_host[2 * i + 1]), q);
   for (int j = 0; j < m; ++j) dg2[j] = powq(diag_dist(d2_host[2 * j], d2_host[2 * j + 1]), q);
-  for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) {
-      double c;
-      if (i < n && j < m) c = powq(linf(d1_host[2 * i], d1_host[2 * i + 1], d2_host[2 * j], d2_host[2 * j + 1]), q);
-      else if (i < n) c = dg1[i];
-      else if (j < m) c = dg2[j];
-      else c = 0.0;
-      C[(size_t)i * N + j] = c;
-    }
-  std::vector<int> asg = hungarian(C, N);
+  auto Cij = [&](int i, int j) {
+    return (double)powq(linf(d1_host[2 * i], d1_host[2 * i + 1], d2_host[2 * j], d2_host[2 * j + 1]), q);
+  };
+  // The (n+m)^2 diagonal-augmented assignment reduces to a rectangular one over the smaller diagram:
+  // cost = sum_i dg1[i] + sum_j dg2[j] + min over partial matchings of sum (C_ij - dg1[i] - dg2[j]).
+  // Rows = points of the smaller diagram, columns = points of the other one plus one "diagonal" column
+  // per row (reduced cost 0). O(r^2 (r + c)) instead of O((n+m)^3).
+  const bool rows_are_d2 = m <= n;
+  const int R = rows_are_d2 ? m : n, Cc = rows_are_d2 ? n : m;
   double cost = 0.0;
-  for (int i = 0; i < N; ++i) cost += C[(size_t)i * N + asg[i]];
+  for (int i = 0; i < n; ++i) cost += dg1[i];
+  for (int j = 0; j < m; ++j) cost += dg2[j];
+  std::vector<int> match_of_d1(n, -1);  // d1 point -> d2 point or -1 (diagonal)
+  if (R > 0) {
+    const int NC = Cc + R;
+    const int N = NC;  // row stride
+    std::vector<double> A((size_t)R * N, 0.0);
+    for (int r = 0; r < R; ++r)
+      for (int c = 0; c < NC; ++c) {
+        double v = 0.0;
+        if (c < Cc) {
+          int i = rows_are_d2 ? c : r, j = rows_are_d2 ? r : c;
+          v = Cij(i, j) - (double)dg1[i] - (double)dg2[j];
+        }
+        A[(size_t)r * N + c] = v;
+      }
+    std::vector<int> asg = hungarian(A, R, NC);
+    for (int r = 0; r < R; ++r) {
+      int c = asg[r];
+      if (c < Cc) {
+        int i = rows_are_d2 ? c : r, j = rows_are_d2 ? r : c;
+        cost += A[(size_t)r * N + c];
+        match_of_d1[i] = j;
+      }
+    }
+  }
   *cost_host = cost;
   for (int i = 0; i < n; ++i) {
-    const int j = asg[i];
+    const int j = match_of_d1[i];
     const float b = d1_host[2 * i], d = d1_host[2 * i + 1];
-    if (j < m) {
+    if (j >= 0) {
       const float e0 = b - d2_host[2 * j], e1 = d - d2_host[2 * j + 1];
       const float M = std::fmax(std::fabs(e0), std::fabs(e1));
       const float coef = (float)(q * std::pow((double)M, q - 1.0));

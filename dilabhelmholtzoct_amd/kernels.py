@@ -100,6 +100,8 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     _require_cuda(dy, x, mean, rstd, w, b, dx, dx2_bf16)
     D = w.numel()
     rows = mean.numel()
+    if D <= 64:
+        nblocks = max(nblocks, 4096)
     nblocks = max(1, min(nblocks, (rows + 3) // 4))
     part = torch.empty((2, nblocks, D), device=dy.device, dtype=torch.float32)
     _lib.call("octsam_layernorm_bwd", ptr(dy), int(dy.dtype == torch.float32), ptr(x),
@@ -147,7 +149,8 @@ def cast_bf16(x, out):
 def colsum(x, rows, cols, out, *, beta=0.0, nblocks=None):
     """out[c] = beta*out[c] + sum_r x[r, c] (x contiguous [rows, cols]); deterministic."""
     if nblocks is None:
-        nblocks = max(1, min(512, rows))
+        lanes = max(1, 256 // max(1, cols // 8))
+        nblocks = max(1, min(1024, (rows + lanes * 16 - 1) // (lanes * 16)))
     part = torch.empty((nblocks, cols), device=x.device, dtype=torch.float32)
     _lib.call("octsam_colsum", ptr(x), _f32(x), rows, cols, ptr(part), nblocks)
     splitk_reduce(part, out, nblocks, beta=beta)
