@@ -316,6 +316,230 @@ int launch(const GemmK& k, int batch, hipStream_t s) {
   return 0;
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Fast path for C = A . B^T with both operands K-contiguous (a_mode 0, b_mode 0), K % BK == 0.
+// Persistent: one 512-thread workgroup per CU walks its XCD's contiguous range of tiles (L2 reuse of the
+// A row panel and of B). Operands stream global -> LDS by global_load_lds_dwordx4 (no VGPR staging) into
+// an NS-stage ring, NS-1 stages in flight behind a counted vmcnt and a raw s_barrier; the ring runs
+// across tile boundaries so the next tile's loads overlap the current epilogue. The XOR chunk swizzle of
+// the LDS image (conflict-free ds_read_b128 fragment reads) is applied on the per-lane SOURCE address.
+// 8 waves = 4 (M) x 2 (N); wave tile 64 x BN/2 of v_mfma_f32_32x32x16_bf16. Rows beyond M / N are
+// clamped to a valid row (their results are never stored).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int BK>
+__device__ __forceinline__ int sw_off(int r, int c) {  // byte offset of 16-B chunk c of row r
+  if constexpr (BK == 64) return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+  else return r * 64 + ((c ^ ((r >> 2) & 3)) << 4);
+}
+
+template <int BK>
+__device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long long ld, int rows, int row0, int k0,
+                                          char* lds, int nrows_tile, int wave, int lane) {
+  constexpr int CPR = BK / 8;          // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;        // rows per wave-instruction (1 KiB)
+  const int ninst = nrows_tile / RPI;
+  for (int j = wave; j < ninst; j += 8) {
+    const int rr = lane / CPR, slot = lane % CPR;
+    const int r = j * RPI + rr;
+    // inverse swizzle: LDS slot `slot` of row r holds logical chunk c
+    int c;
+    if constexpr (BK == 64) c = slot ^ ((r >> 1) & 7);
+    else c = slot ^ ((r >> 2) & 3);
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const bf16* g = src + (long long)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(lds + j * 1024), 16, 0, 0);
+  }
+}
+
+// Fast epilogue (beta == 0, bf16 C, N and ldc even, bf16 residual): no load is issued between stores,
+// so a store never waits on another store's completion. Adjacent lanes trade one value with a DPP quad
+// swap so each lane writes a bf16x2 (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n).
+// Loads are hoisted into two batches (bias + row map, then residual) before any store.
+template <int NI, int NJ>
+__device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][NJ], int bz, int row0, int col0,
+                                              int lane) {
+  bf16* Cb = (bf16*)p.C + bz * p.sC;
+  const bf16* Rb = p.R ? (const bf16*)p.R + bz * p.sR : nullptr;
+  const bool odd = lane & 1;
+  const int ncol = lane & 31;
+  float bv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = col0 + j * 32 + ncol;
+    bv[j] = (p.bias && n < p.N) ? p.bias[n] : 0.0f;
+  }
+  // row handled by this lane for pair t of fragment row-block i
+  int om[NI][8];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int r0 = 2 * t;
+      const int m = row0 + i * 32 + (r0 & 3) + 8 * (r0 >> 2) + 4 * (lane >> 5) + (odd ? 1 : 0);
+      om[i][t] = m < p.M ? (p.row_map ? p.row_map[m] : m) : -1;
+    }
+  uint32_t rv[NI][NJ][8];
+  if (Rb) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = col0 + j * 32 + (ncol & ~1);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int o = om[i][t];
+          rv[i][j][t] = (o >= 0 && c < p.N)
+                            ? *(const uint32_t*)(Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
+        }
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = col0 + j * 32 + (ncol & ~1);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        float v0 = acc[i][j][2 * t] * p.alpha + bv[j];
+        float v1 = acc[i][j][2 * t + 1] * p.alpha + bv[j];
+        if (p.act == OCTSAM_ACT_RELU) {
+          v0 = fmaxf(v0, 0.0f);
+          v1 = fmaxf(v1, 0.0f);
+        } else if (p.act == OCTSAM_ACT_GELU) {
+          v0 = gelu_erf(v0);
+          v1 = gelu_erf(v1);
+        }
+        const float send = odd ? v0 : v1;
+        const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
+                                                                              0xF, 0xF, false));
+        float lo = odd ? recv : v0, hi = odd ? v1 : recv;
+        if (Rb) {
+          const uint32_t r = rv[i][j][t];
+          lo += __builtin_bit_cast(float, r << 16);
+          hi += __builtin_bit_cast(float, r & 0xffff0000u);
+        }
+        const int o = om[i][t];
+        if (o >= 0 && c < p.N) {
+          bf16x2 w;
+          w[0] = (bf16)lo;
+          w[1] = (bf16)hi;
+          *(bf16x2*)(Cb + (long long)o * p.ldc + c) = w;
+        }
+      }
+    }
+}
+
+template <int BN_, int BK, int NS>
+__global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
+  constexpr int BM_ = 256;
+  constexpr int A_BYTES = BM_ * BK * 2, B_BYTES = BN_ * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int NJ = BN_ / 64;  // 32-wide fragments per wave in N (wave tile 64 x BN/2)
+  constexpr int CPR = BK / 8, RPI = 64 / CPR;
+  constexpr int GL_PER_WAVE = (BM_ / RPI + BN_ / RPI) / 8;
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int ntiles = per_batch * batch;
+  const int nxcd_wg = gridDim.x >> 3;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int tper = (ntiles + 7) >> 3;
+  const int tbeg = xcd * tper, tend = min(ntiles, tbeg + tper);
+  const int first = tbeg + loc;
+  const int mycnt = first < tend ? (tend - first + nxcd_wg - 1) / nxcd_wg : 0;
+  const int nk = p.K / BK;
+  const int total = mycnt * nk;
+  if (total == 0) return;
+
+  auto tile_of = [&](int i, int& bz, int& row0, int& col0) {
+    int t = first + i * nxcd_wg;
+    bz = t / per_batch;
+    int r = t - bz * per_batch;
+    int tm = r / p.tiles_n, tn = r - tm * p.tiles_n;
+    row0 = tm * BM_;
+    col0 = tn * BN_;
+  };
+  auto issue = [&](int g) {
+    int i = g / nk, kt = g - i * nk;
+    int bz, r0, c0;
+    tile_of(i, bz, r0, c0);
+    char* st = gsm + (g % NS) * STAGE;
+    glds_tile<BK>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
+    glds_tile<BK>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
+  };
+
+  f32x16 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x16)0.0f;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < total) issue(s);
+  for (int g = 0; g < total; ++g) {
+    // wait for stage g: leave the younger (NS-2) stages in flight
+    const int ahead = min(NS - 2, total - 1 - g);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL_PER_WAVE) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL_PER_WAVE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (g + NS - 1 < total) issue(g + NS - 1);
+    const char* sa = gsm + (g % NS) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ch = kk * 2 + (lane >> 5);
+      bf16x8 af[2], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sa + sw_off<BK>(wm * 64 + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = *(const bf16x8*)(sb + sw_off<BK>(wn * (BN_ / 2) + j * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (g % nk == nk - 1) {
+      int bz, r0, c0;
+      tile_of(g / nk, bz, r0, c0);
+      epilogue_fast<2, NJ>(p, acc, bz, r0 + wm * 64, c0 + wn * (BN_ / 2), lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x16)0.0f;
+    }
+  }
+}
+
+template <int BN_, int BK, int NS>
+int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  constexpr int STAGE = (256 + BN_) * BK * 2;
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + BN_ - 1) / BN_;
+  static int n_cu = 0;
+  if (!n_cu) {
+    (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<BN_, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        NS * STAGE);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+  }
+  const int ntiles = g.tiles_m * g.tiles_n * a->batch;
+  int grid = ((n_cu + 7) / 8) * 8;
+  while (grid > 8 && grid / 2 >= ntiles) grid /= 2;
+  hipLaunchKernelGGL((gemm_glds_kernel<BN_, BK, NS>), dim3(grid), dim3(512), NS * STAGE, s, g, a->batch);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
 __global__ void splitk_reduce_kernel(const float* part, float* out, long long n, int splits, float beta) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -325,7 +549,38 @@ __global__ void splitk_reduce_kernel(const float* part, float* out, long long n,
   out[i] = (beta != 0.0f ? beta * out[i] : 0.0f) + s;
 }
 
+// Vectorised variant: 64 float4 columns x 4 split lanes per block, fixed-order LDS combine.
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float4* __restrict__ part, float4* __restrict__ out,
+                                                             long long n4, int splits, float beta) {
+  __shared__ float4 red[4][64];
+  const int c = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+#pragma unroll 4
+    for (int j = lane; j < splits; j += 4) {
+      float4 v = part[(long long)j * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[lane][c] = s;
+  __syncthreads();
+  if (lane == 0 && i < n4) {
+    float4 r = red[0][c];
+#pragma unroll
+    for (int l = 1; l < 4; ++l) { r.x += red[l][c].x; r.y += red[l][c].y; r.z += red[l][c].z; r.w += red[l][c].w; }
+    if (beta != 0.0f) {
+      float4 o = out[i];
+      r.x += beta * o.x; r.y += beta * o.y; r.z += beta * o.z; r.w += beta * o.w;
+    }
+    out[i] = r;
+  }
+}
+
 }  // namespace
+
+static int g_use_glds = 1;
+extern "C" void octsam_gemm_set_fast_path(int32_t enable) { g_use_glds = enable; }
 
 extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   OCTSAM_CHECK_ARG(a != nullptr, "octsam_gemm: null args");
@@ -363,6 +618,15 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   k.tiles_n = (a->N + BN - 1) / BN;
   hipStream_t s = (hipStream_t)stream;
   const int am = a->a_mode, bm = a->b_mode;
+  const bool fast_epi = a->beta == 0.0f && !a->c_f32 && !a->C_pre && (a->N & 1) == 0 && (a->ldc & 1) == 0 &&
+                        ((uintptr_t)a->C & 3) == 0 &&
+                        (!a->R || (!a->r_f32 && (a->ldr & 1) == 0 && ((uintptr_t)a->R & 3) == 0));
+  if (am == 0 && bm == 0 && a->K % 64 == 0 && a->a_blk == 0 && a->M >= 1024 && g_use_glds && fast_epi &&
+      ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && (a->lda & 7) == 0 && (a->ldb & 7) == 0) {
+    if (g_use_glds == 2) return launch_glds<128, 64, 3>(k, a, s);
+    if (g_use_glds == 3) return launch_glds<256, 32, 4>(k, a, s);
+    return launch_glds<256, 64, 2>(k, a, s);
+  }
   if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);
   if (am == 0 && bm == 1) return launch<0, 1>(k, a->batch, s);
   if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);
@@ -378,6 +642,13 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
 extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
                                     void* stream) {
   OCTSAM_CHECK_ARG(partials && out && n > 0 && splits > 0, "octsam_splitk_reduce: bad args");
+  if (n % 4 == 0 && ((uintptr_t)partials & 15) == 0 && ((uintptr_t)out & 15) == 0 && splits >= 4) {
+    long long n4 = n / 4;
+    hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)partials, (float4*)out, n4, splits, beta);
+    OCTSAM_LAUNCH_CHECK("octsam_splitk_reduce");
+    return 0;
+  }
   long long blocks = (n + 255) / 256;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, partials, out,
                      n, splits, beta);

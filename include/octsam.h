@@ -75,6 +75,8 @@ typedef struct octsam_gemm_args {
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);
+/* enable (1, default) / disable (0) the LDS-DMA 256x128 fast path of octsam_gemm (A/B testing) */
+void octsam_gemm_set_fast_path(int32_t enable);
 
 /* out[i] = sum_{s<splits} partials[s*n+i] + beta*out[i]  (fp32; deterministic split-K combine) */
 int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta, void* stream);
