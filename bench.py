@@ -29,6 +29,10 @@ METRIC = "train imgs/sec (1024² OCT, vit-base, top-loss on) + val Dice; 1→8 G
 MI355X_BF16_DENSE_TFLOPS = 2500.0  # /opt/skills/guides/MI355X_MICROARCH.md (dense, no sparsity)
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -103,14 +107,19 @@ def cpu_baseline(args, batch_cpu):
     """CPU oracle step (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE/topo + Adam) on a
     bounded sample (1 image, all its prompts), timed on this host's cores."""
     from oracle.step_ref import CpuReferenceStep
+    # the GPU box shows the whole machine's CPUs; this job's share is OMP_NUM_THREADS (16 there)
     ncores = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    ncores = min(ncores, share) if share > 0 else min(ncores, 16)
     torch.set_num_threads(ncores)
     step = CpuReferenceStep(args.model, topological=bool(args.top), seed=0)
     one = {k: (v[:1] if isinstance(v, torch.Tensor) and v.dim() > 0 else v) for k, v in batch_cpu.items()}
     step.step(one)  # warm-up
+    log(f"cpu baseline: warm-up done on {ncores} threads")
     t0 = time.time()
     for _ in range(args.cpu_steps):
         step.step(one)
+        log(f"cpu baseline: step {time.time() - t0:.1f} s")
     dt = time.time() - t0
     n_prompts = int(one["gt_u8"].shape[1])
     return {"value": round(args.cpu_steps / dt, 5), "unit": "imgs/s", "cores": torch.get_num_threads(),
@@ -156,9 +165,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    log(f"rank {rank}: N={N} prompts/image, warm-up")
     for _ in range(args.warmup):
         step.step(batch)
     barrier()
+    log(f"rank {rank}: timing {args.steps} steps")
     timer = GemmEventTimer() if not args.no_events else None
     if timer:
         timer.__enter__()
@@ -193,6 +204,7 @@ def main():
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / (dt * 1e3), 4)}
 
+    log(f"rank {rank}: {dt * 1e3 / args.steps:.2f} ms/step")
     val_dice = None
     if args.val and rank == 0:
         vb = data.to_device_batch(make_batch(argparse.Namespace(batch=args.val, prompt=args.prompt), 999, device,
