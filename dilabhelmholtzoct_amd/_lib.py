@@ -44,6 +44,7 @@ _SIGNATURES = {
     "octsam_last_error": (ctypes.c_char_p, []),
     "octsam_gemm": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
     "octsam_gemm_set_fast_path": (None, [c_int32]),
+    "octsam_gemm_last_path": (c_int32, []),
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
     "octsam_cubical_ph": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),

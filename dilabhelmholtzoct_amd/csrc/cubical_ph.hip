@@ -191,7 +191,7 @@ __device__ void h0_wave(Smem& s, const Map& m, int ne) {
     int pos = (int)(uint32_t)ek;
     int u = 0, v = 0;
     if (valid) {
-      int X = pos % m.W2, Y = pos / m.W2;
+      int X = pos % m.W2;
       int pu, pv;
       if (X & 1) { pu = pos - 1; pv = pos + 1; } else { pu = pos - m.W2; pv = pos + m.W2; }
       u = (pu % m.W2) / 2 + (m.W + 1) * ((pu / m.W2) / 2);

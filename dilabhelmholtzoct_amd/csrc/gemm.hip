@@ -354,15 +354,38 @@ __device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long lon
   }
 }
 
-// Fast epilogue (beta == 0, bf16 C, N and ldc even, bf16 residual): no load is issued between stores,
-// so a store never waits on another store's completion. Adjacent lanes trade one value with a DPP quad
-// swap so each lane writes a bf16x2 (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n).
-// Loads are hoisted into two batches (bias + row map, then residual) before any store.
-template <int NI, int NJ>
+// Fast epilogue: adjacent lanes trade one value with a DPP quad swap so each lane owns two adjacent
+// columns of one row (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n) and writes them with one
+// 4-B (bf16x2) or 8-B (float2) store. Loads are hoisted ahead of the stores so a store never waits on an
+// earlier store's completion (vmcnt counts both): bias + row map first, then a bf16 residual for the whole
+// wave tile; an fp32 residual or a beta*C read is loaded per 32-column group (one wait per group).
+// Requires N, ldc (and ldr) even and 4/8-B aligned C / R / C_pre (checked on the host).
+__device__ __forceinline__ float2 ld_pair(const void* base, long long idx, bool f32) {
+  if (f32) return *(const float2*)((const float*)base + idx);
+  const uint32_t r = *(const uint32_t*)((const bf16*)base + idx);
+  return make_float2(__builtin_bit_cast(float, r << 16), __builtin_bit_cast(float, r & 0xffff0000u));
+}
+__device__ __forceinline__ void st_pair(void* base, long long idx, bool f32, float lo, float hi) {
+  if (f32) {
+    *(float2*)((float*)base + idx) = make_float2(lo, hi);
+  } else {
+    bf16x2 w;
+    w[0] = (bf16)lo;
+    w[1] = (bf16)hi;
+    *(bf16x2*)((bf16*)base + idx) = w;
+  }
+}
+__device__ __forceinline__ float dpp_swap1(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+
+template <int NI, int NJ, bool LATE>
 __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][NJ], int bz, int row0, int col0,
                                               int lane) {
-  bf16* Cb = (bf16*)p.C + bz * p.sC;
-  const bf16* Rb = p.R ? (const bf16*)p.R + bz * p.sR : nullptr;
+  const int esz_c = p.c_f32 ? 4 : 2;
+  char* Cb = (char*)p.C + bz * p.sC * esz_c;
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
   const bool odd = lane & 1;
   const int ncol = lane & 31;
   float bv[NJ];
@@ -371,7 +394,6 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
     const int n = col0 + j * 32 + ncol;
     bv[j] = (p.bias && n < p.N) ? p.bias[n] : 0.0f;
   }
-  // row handled by this lane for pair t of fragment row-block i
   int om[NI][8];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
@@ -381,8 +403,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
       const int m = row0 + i * 32 + (r0 & 3) + 8 * (r0 >> 2) + 4 * (lane >> 5) + (odd ? 1 : 0);
       om[i][t] = m < p.M ? (p.row_map ? p.row_map[m] : m) : -1;
     }
-  uint32_t rv[NI][NJ][8];
-  if (Rb) {
+  uint32_t rv[LATE ? 1 : NI][LATE ? 1 : NJ][8];
+  if (!LATE && Rb) {
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -391,48 +413,70 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           const int o = om[i][t];
-          rv[i][j][t] = (o >= 0 && c < p.N)
-                            ? *(const uint32_t*)(Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
+          rv[LATE ? 0 : i][LATE ? 0 : j][t] = (o >= 0 && c < p.N)
+                            ? *(const uint32_t*)((const bf16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
         }
       }
   }
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
+  for (int j = 0; j < NJ; ++j) {
+    const int c = col0 + j * 32 + (ncol & ~1);
+    float2 lr[LATE ? NI : 1][8], lc[LATE ? NI : 1][8];
+    if constexpr (LATE) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = col0 + j * 32 + (ncol & ~1);
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int o = om[i][t];
+          const bool ok = o >= 0 && c < p.N;
+          lr[i][t] = (Rb && ok) ? ld_pair(Rb, remap(o, p.r_blk, p.r_rep) * p.ldr + c, p.r_f32) : make_float2(0.f, 0.f);
+          lc[i][t] = (p.beta != 0.0f && ok) ? ld_pair(Cb, (long long)o * p.ldc + c, p.c_f32) : make_float2(0.f, 0.f);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        float v0 = acc[i][j][2 * t] * p.alpha + bv[j];
-        float v1 = acc[i][j][2 * t + 1] * p.alpha + bv[j];
-        if (p.act == OCTSAM_ACT_RELU) {
-          v0 = fmaxf(v0, 0.0f);
-          v1 = fmaxf(v1, 0.0f);
-        } else if (p.act == OCTSAM_ACT_GELU) {
-          v0 = gelu_erf(v0);
-          v1 = gelu_erf(v1);
-        }
-        const float send = odd ? v0 : v1;
-        const float recv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1,
-                                                                              0xF, 0xF, false));
+        float v0 = acc[i][j][2 * t] * p.alpha;
+        float v1 = acc[i][j][2 * t + 1] * p.alpha;
+        // pair layout first, so the beta*C / residual reads use the stored pair order
+        const float recv = dpp_swap1(odd ? v0 : v1);
         float lo = odd ? recv : v0, hi = odd ? v1 : recv;
-        if (Rb) {
-          const uint32_t r = rv[i][j][t];
-          lo += __builtin_bit_cast(float, r << 16);
-          hi += __builtin_bit_cast(float, r & 0xffff0000u);
+        const float b_lo = odd ? dpp_swap1(bv[j]) : bv[j];
+        const float b_hi = odd ? bv[j] : dpp_swap1(bv[j]);
+        if constexpr (LATE) {
+          lo += p.beta * lc[i][t].x;
+          hi += p.beta * lc[i][t].y;
         }
+        lo += b_lo;
+        hi += b_hi;
         const int o = om[i][t];
-        if (o >= 0 && c < p.N) {
-          bf16x2 w;
-          w[0] = (bf16)lo;
-          w[1] = (bf16)hi;
-          *(bf16x2*)(Cb + (long long)o * p.ldc + c) = w;
+        const bool ok = o >= 0 && c < p.N;
+        const long long ci = (long long)o * p.ldc + c;
+        if (Pb && ok) st_pair(Pb, ci, p.pre_f32, lo, hi);
+        if (p.act == OCTSAM_ACT_RELU) {
+          lo = fmaxf(lo, 0.0f);
+          hi = fmaxf(hi, 0.0f);
+        } else if (p.act == OCTSAM_ACT_GELU) {
+          lo = gelu_erf(lo);
+          hi = gelu_erf(hi);
         }
+        if (Rb) {
+          if constexpr (LATE) {
+            lo += lr[i][t].x;
+            hi += lr[i][t].y;
+          } else {
+            const uint32_t r = rv[LATE ? 0 : i][LATE ? 0 : j][t];
+            lo += __builtin_bit_cast(float, r << 16);
+            hi += __builtin_bit_cast(float, r & 0xffff0000u);
+          }
+        }
+        if (ok) st_pair(Cb, ci, p.c_f32, lo, hi);
       }
-    }
+  }
 }
 
-template <int BN_, int BK, int NS>
+template <int BN_, int BK, int NS, bool LATE>
 __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   constexpr int BM_ = 256;
   constexpr int A_BYTES = BM_ * BK * 2, B_BYTES = BN_ * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -508,7 +552,7 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
     if (g % nk == nk - 1) {
       int bz, r0, c0;
       tile_of(g / nk, bz, r0, c0);
-      epilogue_fast<2, NJ>(p, acc, bz, r0 + wm * 64, c0 + wn * (BN_ / 2), lane);
+      epilogue_fast<2, NJ, LATE>(p, acc, bz, r0 + wm * 64, c0 + wn * (BN_ / 2), lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -517,15 +561,15 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   }
 }
 
-template <int BN_, int BK, int NS>
-int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+template <int BN_, int BK, int NS, bool LATE>
+int launch_glds_t(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   constexpr int STAGE = (256 + BN_) * BK * 2;
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + BN_ - 1) / BN_;
   static int n_cu = 0;
   if (!n_cu) {
-    (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<BN_, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<BN_, BK, NS, LATE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         NS * STAGE);
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -535,9 +579,16 @@ int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   const int ntiles = g.tiles_m * g.tiles_n * a->batch;
   int grid = ((n_cu + 7) / 8) * 8;
   while (grid > 8 && grid / 2 >= ntiles) grid /= 2;
-  hipLaunchKernelGGL((gemm_glds_kernel<BN_, BK, NS>), dim3(grid), dim3(512), NS * STAGE, s, g, a->batch);
+  hipLaunchKernelGGL((gemm_glds_kernel<BN_, BK, NS, LATE>), dim3(grid), dim3(512), NS * STAGE, s, g, a->batch);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
+}
+
+template <int BN_, int BK, int NS>
+int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  // fp32 residual / beta*C epilogue: the 256x128 tile (the 256x256 one would spill)
+  if ((a->R && a->r_f32) || a->beta != 0.0f) return launch_glds_t<128, 64, 3, true>(k0, a, s);
+  return launch_glds_t<BN_, BK, NS, false>(k0, a, s);
 }
 
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
@@ -580,7 +631,9 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float4* __res
 }  // namespace
 
 static int g_use_glds = 1;
+static thread_local int t_last_path = 0;
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) { g_use_glds = enable; }
+extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
 
 extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   OCTSAM_CHECK_ARG(a != nullptr, "octsam_gemm: null args");
@@ -618,15 +671,17 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   k.tiles_n = (a->N + BN - 1) / BN;
   hipStream_t s = (hipStream_t)stream;
   const int am = a->a_mode, bm = a->b_mode;
-  const bool fast_epi = a->beta == 0.0f && !a->c_f32 && !a->C_pre && (a->N & 1) == 0 && (a->ldc & 1) == 0 &&
-                        ((uintptr_t)a->C & 3) == 0 &&
-                        (!a->R || (!a->r_f32 && (a->ldr & 1) == 0 && ((uintptr_t)a->R & 3) == 0));
+  const bool fast_epi = (a->N & 1) == 0 && (a->ldc & 1) == 0 && ((uintptr_t)a->C & 7) == 0 &&
+                        (!a->C_pre || ((uintptr_t)a->C_pre & 7) == 0) &&
+                        (!a->R || ((a->ldr & 1) == 0 && ((uintptr_t)a->R & 7) == 0));
   if (am == 0 && bm == 0 && a->K % 64 == 0 && a->a_blk == 0 && a->M >= 1024 && g_use_glds && fast_epi &&
       ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && (a->lda & 7) == 0 && (a->ldb & 7) == 0) {
+    t_last_path = 1;
     if (g_use_glds == 2) return launch_glds<128, 64, 3>(k, a, s);
     if (g_use_glds == 3) return launch_glds<256, 32, 4>(k, a, s);
     return launch_glds<256, 64, 2>(k, a, s);
   }
+  t_last_path = 0;
   if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);
   if (am == 0 && bm == 1) return launch<0, 1>(k, a->batch, s);
   if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);

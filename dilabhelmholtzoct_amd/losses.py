@@ -188,7 +188,7 @@ class DiceCELoss:
 
 
 # ------------------------------------------------------------------------ topological loss
-def topo_entries(B: int, N: int, mode: str = "first"):
+def topo_entries(B: int, N: int, mode: str = "first", global_batch: int | None = None):
     """Which (b, n) maps each loss entry of topo_loss covers, after `.squeeze()` + CubicalComplex
     nesting + torch_topological.batch_iter(dim=feat_d) (topological_loss.py:62-76):
       B == 1           -> one entry per prompt (nesting level 2)
@@ -196,8 +196,12 @@ def topo_entries(B: int, N: int, mode: str = "first"):
       B > 1 and N > 1  -> one entry per image (nesting level 3); mode "first": only prompt 0 of the
                           image (the upstream handler keeps the first channel),
                           mode "all": every prompt of the image (costs summed before the 1/q power).
-    batch_iter's nesting semantics are unpinned (torch_topological absent)."""
-    if B == 1:
+    batch_iter's nesting semantics are unpinned (torch_topological absent).
+    global_batch: the batch the single-process reference would see (data parallel: the sum over
+    ranks); the nesting level follows it, so a rank holding one image of a larger global batch still
+    uses the per-image rule."""
+    GB = B if global_batch is None else global_batch
+    if GB == 1:
         return [[n] for n in range(N)]
     if N == 1:
         return [[b] for b in range(B)]
@@ -207,14 +211,17 @@ def topo_entries(B: int, N: int, mode: str = "first"):
 
 
 def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch.Tensor | None, *, lamda=0.1,
-                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=1024, logits=True):
+                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=1024, logits=True,
+                          global_batch: int | None = None):
     """Topological loss value (float) and, when dmask is given, its gradient added into dmask.
     masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64)."""
     if lamda == 0.0:
         return 0.0
     B, N, H, W = masks.shape
     dev = masks.device
-    entries = topo_entries(B, N, mode)
+    entries = topo_entries(B, N, mode, global_batch)
+    if not entries:
+        return 0.0
     maps = sorted({m for e in entries for m in e})
     Kn = len(maps)
     midx = torch.tensor(maps, dtype=torch.int32, device=dev)

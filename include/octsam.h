@@ -75,8 +75,11 @@ typedef struct octsam_gemm_args {
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);
-/* enable (1, default) / disable (0) the LDS-DMA 256x128 fast path of octsam_gemm (A/B testing) */
+/* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing) */
 void octsam_gemm_set_fast_path(int32_t enable);
+/* 1 if the calling thread's last octsam_gemm launched the persistent global_load_lds kernel
+   (gemm_glds_kernel), 0 for the generic tile kernel. Used to attribute per-kernel timings. */
+int32_t octsam_gemm_last_path(void);
 
 /* out[i] = sum_{s<splits} partials[s*n+i] + beta*out[i]  (fp32; deterministic split-K combine) */
 int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta, void* stream);

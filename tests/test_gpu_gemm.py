@@ -117,3 +117,54 @@ def test_splitk_reduce(cuda):
     out = torch.ones(1000, device=cuda)
     kernels.splitk_reduce(part, out, 5, beta=1.0)
     assert torch.allclose(out, part.sum(0) + 1, atol=1e-5)
+
+
+@pytest.mark.parametrize("c_f32", [False, True])
+@pytest.mark.parametrize("resid", [None, "bf16", "f32"])
+@pytest.mark.parametrize("beta", [0.0, 1.5])
+@pytest.mark.parametrize("pre", [None, "bf16", "f32"])
+def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
+    """The persistent LDS-DMA kernel (a_mode = b_mode = 0, M >= 1024, K % 64 == 0) with every epilogue
+    option, ragged M/N tiles, batch strides and a row map; the generic kernel and torch fp32 as references."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    Bt, M, N, K = 2, 1100, 392, 192
+    g = torch.Generator().manual_seed(int(c_f32) * 100 + int(beta * 10) + len(str(resid)) + len(str(pre)))
+    A = torch.randn(Bt, M, K, generator=g).to(cuda, torch.bfloat16)
+    W = torch.randn(Bt, N, K, generator=g).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    cdt = torch.float32 if c_f32 else torch.bfloat16
+    C0 = torch.randn(Bt, M, N, generator=g).to(cuda, cdt)
+    R = None if resid is None else torch.randn(Bt, M, N, generator=g).to(cuda, torch.float32 if resid == "f32"
+                                                                          else torch.bfloat16)
+    rm = torch.randperm(M, generator=g).to(torch.int32)
+    rm[::7] = -1
+    rm = rm.to(cuda)
+    outs = []
+    for fast in (1, 0):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = C0.clone()
+        pout = None if pre is None else torch.zeros(Bt, M, N, device=cuda,
+                                                    dtype=torch.float32 if pre == "f32" else torch.bfloat16)
+        kw = dict(M=M, N=N, K=K, out=out, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c=M * N, bias=bias,
+                  act=2, beta=beta, alpha=0.75, pre_out=pout, row_map=rm)
+        if R is not None:
+            kw.update(residual=R, stride_r=M * N)
+        kernels.gemm(A, W, **kw)
+        assert lib.octsam_gemm_last_path() == fast
+        outs.append((out, pout))
+    lib.octsam_gemm_set_fast_path(1)
+    keep = (rm >= 0).nonzero().flatten()
+    dst = rm[keep].long()
+    pre_ref = 0.75 * torch.bmm(A.float(), W.float().transpose(1, 2))[:, keep] + beta * C0.float()[:, dst] + bias
+    ref = F.gelu(pre_ref) + (R.float()[:, dst] if R is not None else 0.0)
+    tol = 1e-5 if c_f32 else 8e-3
+    for out, pout in outs:
+        assert _rel(out[:, dst], ref) < tol
+        if pout is not None:
+            assert _rel(pout[:, dst], pre_ref) < (1e-5 if pre == "f32" else 8e-3)
+    # rows dropped by the row map keep their previous contents
+    drop = torch.ones(M, dtype=torch.bool, device=cuda)
+    drop[dst] = False
+    assert torch.equal(outs[0][0][:, drop], C0[:, drop])
+    assert _rel(outs[0][0], outs[1][0]) < tol
