@@ -354,6 +354,45 @@ __device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long lon
   }
 }
 
+// k-major operand (the operand stored [K][X], X = M or N contiguous: dY^T / X^T of weight gradients,
+// a weight used as W rather than W^T). LDS image: per 128-column half a [64 k-rows][128] tile with 256-B
+// rows and chunk swizzle f(r) = ((r&3)<<2) | ((r>>2)&3); fragments come out of ds_read_b64_tr_b16
+// (gfx950 LDS transpose read), conflict-free on this image. X % 8 == 0 and ld % 8 == 0 (host-checked);
+// columns past X are clamped to the last chunk (their results are never stored).
+__device__ __forceinline__ int km_off(int r, int ch) { return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4); }
+
+template <int TX>
+__device__ __forceinline__ void glds_tile_km(const bf16* __restrict__ src, long long ld, int xdim, int x0, int k0,
+                                             char* lds, int wave, int lane) {
+  constexpr int NINST = TX / 8;  // 64 rows * TX * 2 B / 1 KiB
+#pragma unroll
+  for (int j = wave; j < NINST; j += 8) {
+    const int h = j >> 4, r = ((j & 15) << 2) + (lane >> 4), slot = lane & 15;
+    const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    int col = x0 + h * 128 + ch * 8;
+    col = col < xdim ? col : xdim - 8;
+    const bf16* g = src + (long long)(k0 + r) * ld + col;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(lds + h * 16384 + (j & 15) * 1024), 16, 0, 0);
+  }
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 32x32x16 MFMA operand (8 consecutive k of row xb + (lane & 31), k from kb + 8*(lane>>5)) from a k-major image
+__device__ __forceinline__ bf16x8 frag_km(const char* img, int xb, int kb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int x = xb + 16 * (g & 1);
+  const int h = x >> 7, c0 = (x & 127) >> 3;
+  const int r0 = kb + 8 * (g >> 1) + q;
+  const char* base = img + h * 16384 + 8 * (pp & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + km_off(r0, c0 + (pp >> 1))));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + km_off(r0 + 4, c0 + (pp >> 1))));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // Fast epilogue: adjacent lanes trade one value with a DPP quad swap so each lane owns two adjacent
 // columns of one row (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n) and writes them with one
 // 4-B (bf16x2) or 8-B (float2) store. Loads are hoisted ahead of the stores so a store never waits on an
@@ -439,11 +478,14 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
       for (int t = 0; t < 8; ++t) {
         float v0 = acc[i][j][2 * t] * p.alpha;
         float v1 = acc[i][j][2 * t + 1] * p.alpha;
-        // pair layout first, so the beta*C / residual reads use the stored pair order
-        const float recv = dpp_swap1(odd ? v0 : v1);
+        // pair layout first, so the beta*C / residual reads use the stored pair order. Every DPP runs
+        // unconditionally in all lanes (a DPP under a divergent select would read inactive lanes).
+        const float send = odd ? v0 : v1;
+        const float recv = dpp_swap1(send);
+        const float bsw = dpp_swap1(bv[j]);
         float lo = odd ? recv : v0, hi = odd ? v1 : recv;
-        const float b_lo = odd ? dpp_swap1(bv[j]) : bv[j];
-        const float b_hi = odd ? bv[j] : dpp_swap1(bv[j]);
+        const float b_lo = odd ? bsw : bv[j];
+        const float b_hi = odd ? bv[j] : bsw;
         if constexpr (LATE) {
           lo += p.beta * lc[i][t].x;
           hi += p.beta * lc[i][t].y;
@@ -476,8 +518,9 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
   }
 }
 
-template <int BN_, int BK, int NS, bool LATE>
+template <int BN_, int BK, int NS, bool LATE, bool AKM, bool BKM>
 __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
+  static_assert(!(AKM || BKM) || BK == 64, "k-major operands use BK = 64");
   constexpr int BM_ = 256;
   constexpr int A_BYTES = BM_ * BK * 2, B_BYTES = BN_ * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NJ = BN_ / 64;  // 32-wide fragments per wave in N (wave tile 64 x BN/2)
@@ -511,8 +554,10 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
     int bz, r0, c0;
     tile_of(i, bz, r0, c0);
     char* st = gsm + (g % NS) * STAGE;
-    glds_tile<BK>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
-    glds_tile<BK>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
+    if constexpr (AKM) glds_tile_km<BM_>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, wave, lane);
+    else glds_tile<BK>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
+    if constexpr (BKM) glds_tile_km<BN_>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, wave, lane);
+    else glds_tile<BK>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
   };
 
   f32x16 acc[2][NJ];
@@ -539,10 +584,15 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
       const int ch = kk * 2 + (lane >> 5);
       bf16x8 af[2], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sa + sw_off<BK>(wm * 64 + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (AKM) af[i] = frag_km(sa, wm * 64 + i * 32, kk * 16, lane);
+        else af[i] = *(const bf16x8*)(sa + sw_off<BK>(wm * 64 + i * 32 + (lane & 31), ch));
+      }
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        bfr[j] = *(const bf16x8*)(sb + sw_off<BK>(wn * (BN_ / 2) + j * 32 + (lane & 31), ch));
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (BKM) bfr[j] = frag_km(sb, wn * (BN_ / 2) + j * 32, kk * 16, lane);
+        else bfr[j] = *(const bf16x8*)(sb + sw_off<BK>(wn * (BN_ / 2) + j * 32 + (lane & 31), ch));
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -561,7 +611,7 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   }
 }
 
-template <int BN_, int BK, int NS, bool LATE>
+template <int BN_, int BK, int NS, bool LATE, bool AKM, bool BKM>
 int launch_glds_t(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   constexpr int STAGE = (256 + BN_) * BK * 2;
   GemmK g = k0;
@@ -569,7 +619,7 @@ int launch_glds_t(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   g.tiles_n = (a->N + BN_ - 1) / BN_;
   static int n_cu = 0;
   if (!n_cu) {
-    (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<BN_, BK, NS, LATE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_glds_kernel<BN_, BK, NS, LATE, AKM, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         NS * STAGE);
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -579,16 +629,16 @@ int launch_glds_t(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   const int ntiles = g.tiles_m * g.tiles_n * a->batch;
   int grid = ((n_cu + 7) / 8) * 8;
   while (grid > 8 && grid / 2 >= ntiles) grid /= 2;
-  hipLaunchKernelGGL((gemm_glds_kernel<BN_, BK, NS, LATE>), dim3(grid), dim3(512), NS * STAGE, s, g, a->batch);
+  hipLaunchKernelGGL((gemm_glds_kernel<BN_, BK, NS, LATE, AKM, BKM>), dim3(grid), dim3(512), NS * STAGE, s, g, a->batch);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
 }
 
-template <int BN_, int BK, int NS>
+template <int BN_, int BK, int NS, bool AKM = false, bool BKM = false>
 int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   // fp32 residual / beta*C epilogue: the 256x128 tile (the 256x256 one would spill)
-  if ((a->R && a->r_f32) || a->beta != 0.0f) return launch_glds_t<128, 64, 3, true>(k0, a, s);
-  return launch_glds_t<BN_, BK, NS, false>(k0, a, s);
+  if ((a->R && a->r_f32) || a->beta != 0.0f) return launch_glds_t<128, 64, 3, true, AKM, BKM>(k0, a, s);
+  return launch_glds_t<BN_, BK, NS, false, AKM, BKM>(k0, a, s);
 }
 
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
@@ -674,11 +724,21 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   const bool fast_epi = (a->N & 1) == 0 && (a->ldc & 1) == 0 && ((uintptr_t)a->C & 7) == 0 &&
                         (!a->C_pre || ((uintptr_t)a->C_pre & 7) == 0) &&
                         (!a->R || ((a->ldr & 1) == 0 && ((uintptr_t)a->R & 7) == 0));
-  if (am == 0 && bm == 0 && a->K % 64 == 0 && a->a_blk == 0 && a->M >= 1024 && g_use_glds && fast_epi &&
-      ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && (a->lda & 7) == 0 && (a->ldb & 7) == 0) {
+  // persistent LDS-DMA kernel: K-contiguous (mode 0) or k-major (mode 1, transposed-read) operands
+  const bool ok_a = (a->lda & 7) == 0 && (am == 0 || (am == 1 && (a->M & 7) == 0 && a->M >= 8));
+  const bool ok_b = (a->ldb & 7) == 0 && (bm == 0 || (bm == 1 && (a->N & 7) == 0 && a->N >= 8));
+  const long long tiles = (long long)((a->M + 255) / 256) * ((a->N + 127) / 128) * a->batch;
+  if (g_use_glds && ok_a && ok_b && a->K % 64 == 0 && a->a_blk == 0 && a->b_blk == 0 && fast_epi &&
+      (a->M >= 1024 || tiles >= 64) && ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 &&
+      (a->batch == 1 || ((a->stride_a & 7) == 0 && (a->stride_b & 7) == 0))) {
     t_last_path = 1;
+    // transposed-read operands need more address registers: the 256x128 tile (no spills)
+    if (am == 1 && bm == 1) return launch_glds<128, 64, 3, true, true>(k, a, s);
+    if (am == 1) return launch_glds<128, 64, 3, true, false>(k, a, s);
+    if (bm == 1) return launch_glds<128, 64, 3, false, true>(k, a, s);
     if (g_use_glds == 2) return launch_glds<128, 64, 3>(k, a, s);
     if (g_use_glds == 3) return launch_glds<256, 32, 4>(k, a, s);
+    if (a->N <= 64) return launch_glds<64, 64, 3>(k, a, s);  // narrow outputs (ConvT 64-channel GEMMs)
     return launch_glds<256, 64, 2>(k, a, s);
   }
   t_last_path = 0;

@@ -241,37 +241,64 @@ class MaskDecoder(nn.Module):
              a2_rows=0, lda=None, ldc=None, pre_out=None, wgroup=None, bgroup=None):
         w = self.W(wname) if wgroup is None else self._group(self.flat_b16, wgroup, C)
         b = self.Bf(bname) if bgroup is None else self._group(self.flat, bgroup, 0)
+        if a_mode == 4 and act == 0 and residual is None and pre_out is None:
+            # (x + pe[m % L]) W^T + b = x W^T + P[m % L] with P = pe W^T + b (L x N, computed once): the
+            # big product runs on the K-contiguous fast path, P enters as a periodic residual
+            N = w.shape[0]
+            P = torch.empty(a2_rows, N, device=out.device, dtype=torch.bfloat16)
+            K.gemm(A2, w, M=a2_rows, N=N, K=w.shape[1], out=P, bias=b, lda=lda)
+            K.gemm(x, w, M=M, N=N, K=w.shape[1], out=out, residual=P, ldr=N, r_remap=(a2_rows, max(1, M // a2_rows)),
+                   lda=lda, ldc=ldc)
+            return out
         K.gemm(x, w, M=M, N=w.shape[0], K=w.shape[1], out=out, bias=b, act=act, residual=residual, r_remap=r_remap,
                a_mode=a_mode, A2=A2, a2_rows=a2_rows, lda=lda, ldc=ldc, pre_out=pre_out)
         return out
 
-    def _dw(self, dy, x, M, out, *, ldy=None, ldx=None, x_add=None, x_add_rows=0, split=None):
-        """out[o, i] = sum_m dy[m, o] * (x[m, i] (+ x_add[m % rows, i])) -> fp32 (deterministic split-K)."""
+    @staticmethod
+    def _pick_split(Mtok, O, I):
+        """Split-K factor for a weight gradient with Mtok reduction rows: enough (O x I tiles) x splits to fill
+        the chip, chunks a multiple of 64 rows when possible (the persistent kernel's K step), >= 32 rows."""
+        tiles = -(-O // 256) * -(-I // 128)
+        aligned = Mtok % 64 == 0
+        best = 1
+        for s in range(1, 513):
+            if Mtok % s:
+                continue
+            ch = Mtok // s
+            if ch < 32:
+                break
+            if aligned and ch % 64:
+                continue
+            best = s
+            if tiles * s >= 256:
+                break
+        return best
+
+    def _dw(self, dy, x, M, out, *, ldy=None, ldx=None, x_add=None, x_add_rows=0, split=None, accumulate=False):
+        """out[o, i] (+)= sum_m dy[m, o] * (x[m, i] (+ x_add[m % rows, i])) -> fp32 (deterministic split-K).
+        The periodic addend (the image PE added to the keys) is folded as dy^T x + S^T x_add with
+        S[p] = sum_j dy[j*rows + p], so the big product is a plain k-major GEMM."""
         O, I = out.shape
         ldy = O if ldy is None else ldy
         ldx = I if ldx is None else ldx
+        if x_add is not None:
+            rows = x_add_rows
+            S = torch.empty(rows, O, device=out.device, dtype=torch.bfloat16)
+            K.group_sum(dy, S, ld_in=ldy, cols=O, groups=1, nper=M // rows, rows_per=rows)
+            self._dw(dy, x, M, out, ldy=ldy, ldx=ldx, accumulate=accumulate)
+            self._dw(S, x_add, rows, out, ldy=O, ldx=ldx, accumulate=True)
+            return out
         if split is None:
-            if x_add is not None:
-                # the periodic addend row is (local k) % rows: every split must start on a period boundary
-                nper = M // x_add_rows
-                split = 1
-                for d in range(1, min(nper, 256) + 1):
-                    if nper % d == 0:
-                        split = d
-            else:
-                split = 1
-                while M // split > 4096 and M % (split * 2) == 0 and split < 256:
-                    split *= 2
-        b_mode = 2 if x_add is not None else 1
+            split = self._pick_split(M, O, I)
+        beta = 1.0 if accumulate else 0.0
         if split == 1:
-            K.gemm(dy, x, M=O, N=I, K=M, out=out, a_mode=1, b_mode=b_mode, lda=ldy, ldb=ldx, B2=x_add,
-                   b2_rows=x_add_rows)
+            K.gemm(dy, x, M=O, N=I, K=M, out=out, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, beta=beta)
             return out
         Ks = M // split
         part = torch.empty((split, O, I), device=out.device, dtype=torch.float32)
-        K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=b_mode, lda=ldy, ldb=ldx, B2=x_add,
-               b2_rows=x_add_rows, batch=split, stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I)
-        K.splitk_reduce(part.view(split, -1), out, split)
+        K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, batch=split,
+               stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I)
+        K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
         return out
 
     def _lin_bwd(self, dy_b, x_b, wname, bname, M, *, dx_out=None, dx_beta=0.0, ldy=None, ldx=None, x_add=None,

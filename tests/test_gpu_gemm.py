@@ -168,3 +168,29 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     drop[dst] = False
     assert torch.equal(outs[0][0][:, drop], C0[:, drop])
     assert _rel(outs[0][0], outs[1][0]) < tol
+
+
+@pytest.mark.parametrize("a_mode,b_mode", [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("shape", [(1104, 392, 192, 2), (256, 256, 128, 64), (128, 264, 64, 40)])
+def test_gemm_fast_path_kmajor(cuda, a_mode, b_mode, shape):
+    """k-major operands (a_mode 1: A stored [K][M]; b_mode 1: B stored [K][N]) through the persistent
+    kernel's LDS transpose reads, incl. the split-K weight-gradient shape (small M x N, many batches)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    M, N, K, Bt = shape
+    g = torch.Generator().manual_seed(M + N + K + 7 * a_mode + 3 * b_mode)
+    A = torch.randn(Bt, M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(Bt, N, K, generator=g).to(torch.bfloat16)
+    Aop = (A if a_mode == 0 else A.transpose(1, 2)).contiguous().to(cuda)
+    Bop = (W if b_mode == 0 else W.transpose(1, 2)).contiguous().to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(Bt, M, N, generator=g).to(cuda, torch.bfloat16)
+    ref = F.relu(torch.bmm(A.float(), W.float().transpose(1, 2)).to(cuda) + bias) + R.float()
+    for fast in (1, 0):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(Bt, M, N, device=cuda, dtype=torch.float32)
+        kernels.gemm(Aop, Bop, M=M, N=N, K=K, out=out, a_mode=a_mode, b_mode=b_mode, batch=Bt, stride_a=M * K,
+                     stride_b=N * K, stride_c=M * N, stride_r=M * N, bias=bias, act=1, residual=R)
+        assert lib.octsam_gemm_last_path() == fast
+        assert _rel(out, ref) < 1e-5, (fast, _rel(out, ref))
+    lib.octsam_gemm_set_fast_path(1)
