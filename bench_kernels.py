@@ -34,7 +34,7 @@ def main():
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         res = {"case": "gemm_nt", "M": M, "N": N, "K": Kd}
         ref = A[-2048:].float() @ W.float().t()
-        for fast in (1, 2, 3, 0):
+        for fast in (1, 5, 0):
             lib.octsam_gemm_set_fast_path(fast)
             ms = timeit(lambda: K.gemm(A, W, M=M, N=N, K=Kd, out=out))
             out.zero_()
@@ -50,10 +50,17 @@ def main():
         qkv = torch.randn(nseq, T, 3 * heads * 64, generator=g).to(dev, torch.bfloat16)
         o = torch.empty(nseq, T, heads * 64, device=dev, dtype=torch.bfloat16)
         Rh = torch.randn(2 * side - 1, 64, device=dev) * 0.02
-        ms = timeit(lambda: K.vit_attention(qkv, o, Rh, Rh, nseq=nseq, side=side, heads=heads))
         fl = 4.0 * nseq * heads * T * T * 64
-        print(json.dumps({"case": "vit_attention", "side": side, "nseq": nseq, "ms": round(ms, 4),
-                          "tflops": round(fl / ms / 1e9, 1)}), flush=True)
+        res = {"case": "vit_attention", "side": side, "nseq": nseq}
+        outs = []
+        for v in (1, 0):
+            lib.octsam_attention_set_variant(v)
+            ms = timeit(lambda: K.vit_attention(qkv, o, Rh, Rh, nseq=nseq, side=side, heads=heads))
+            res[f"v{v}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
+            outs.append(o.float().clone())
+        lib.octsam_attention_set_variant(1)
+        res["v1_vs_v0_maxdiff"] = (outs[0] - outs[1]).abs().max().item()
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -328,6 +328,14 @@ int launch(const GemmK& k, int batch, hipStream_t s) {
 // clamped to a valid row (their results are never stored).
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// raw s_barrier with compiler fences: the intrinsic alone does not stop LDS reads / LDS-DMA issue
+// from being moved across it
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int BK>
 __device__ __forceinline__ int sw_off(int r, int c) {  // byte offset of 16-B chunk c of row r
   if constexpr (BK == 64) return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL_PER_WAVE) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL_PER_WAVE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
     if (g + NS - 1 < total) issue(g + NS - 1);
     const char* sa = gsm + (g % NS) * STAGE;
     const char* sb = sa + A_BYTES;
@@ -639,6 +647,354 @@ int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   // fp32 residual / beta*C epilogue: the 256x128 tile (the 256x256 one would spill)
   if ((a->R && a->r_f32) || a->beta != 0.0f) return launch_glds_t<128, 64, 3, true, AKM, BKM>(k0, a, s);
   return launch_glds_t<BN_, BK, NS, false, AKM, BKM>(k0, a, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 8-phase NT GEMM (a_mode 0, b_mode 0, K % 64 == 0): 256x256 tile, BK = 64, 8 waves as 2 (M) x 4 (N),
+// wave tile 128 x 64 of v_mfma_f32_16x16x32_bf16, one tile per workgroup (XCD-contiguous tile order).
+// Two LDS buffers (K-tiles alternate); each buffer is split into regions by the phase that reads them:
+// A-lo / A-hi = rows 0-63 / 64-127 of each wave-row block, B-n0 / B-n1 = cols 0-31 / 32-63 of each
+// wave-column block. A K-tile is four phases, one 64x32 quadrant of the wave tile x K = 64 (16 MFMAs)
+// each: Q(0,0) reads A-lo + B-n0, Q(0,1) B-n1, Q(1,0) A-hi, Q(1,1) nothing. A region is reloaded by
+// global_load_lds two phases after its last read and read ~6 phases after its load is issued; counted
+// vmcnt before the first barrier of the phase preceding the read, raw s_barrier, and the two wave rows
+// run one barrier apart so one row's MFMAs overlap the other's LDS reads.
+namespace ph8 {
+constexpr int BUF = 65536;  // A [256][64] + B [256][64] bf16
+
+// region 0 A-lo, 1 A-hi, 2 B-n0, 3 B-n1: 128 rows x 128 B = 16 instructions of 8 rows, 2 per wave
+__device__ __forceinline__ void load_region(const GemmK& p, const bf16* A, const bf16* B, int region, int row0,
+                                            int col0, int k0, char* buf, int wave, int lane) {
+  const bool isA = region < 2;
+  const bf16* src = isA ? A : B;
+  const long long ld = isA ? p.lda : p.ldb;
+  const int lim = isA ? p.M : p.N, g0 = isA ? row0 : col0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = wave * 2 + u;
+    const int rbase = isA ? (j >> 3) * 128 + (region & 1) * 64 + (j & 7) * 8
+                          : (j >> 2) * 64 + (region & 1) * 32 + (j & 3) * 8;
+    const int r = rbase + (lane >> 3), slot = lane & 7;
+    const int c = slot ^ ((r >> 1) & 7);
+    int gr = g0 + r;
+    gr = gr < lim ? gr : lim - 1;
+    const bf16* g = src + (long long)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(buf + (isA ? 0 : 32768) + rbase * 128), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag(const char* img, int row, int kc) {
+  return *(const bf16x8*)(img + sw_off<64>(row, kc));
+}
+
+// lane: col n = lane & 15, rows 4*(lane>>4) + i. Pairs (i, i+1) of adjacent lanes are merged by a DPP
+// swap as in epilogue_fast: even lane -> row r (cols n, n+1), odd lane -> row r+1 (cols n-1, n).
+template <bool LATE>
+__device__ __forceinline__ void epilogue16(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0, int lane) {
+  const int esz_c = p.c_f32 ? 4 : 2;
+  char* Cb = (char*)p.C + bz * p.sC * esz_c;
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
+  const bool odd = lane & 1;
+  float bv[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = col0 + ni * 16 + (lane & 15);
+    bv[ni] = (p.bias && n < p.N) ? p.bias[n] : 0.0f;
+  }
+  int om[8][2];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int m = row0 + mi * 16 + 4 * (lane >> 4) + 2 * t + (odd ? 1 : 0);
+      om[mi][t] = m < p.M ? (p.row_map ? p.row_map[m] : m) : -1;
+    }
+  uint32_t rv[LATE ? 1 : 8][LATE ? 1 : 4][2];
+  if (!LATE && Rb) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int c = col0 + ni * 16 + ((lane & 15) & ~1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int o = om[mi][t];
+          rv[LATE ? 0 : mi][LATE ? 0 : ni][t] =
+              (o >= 0 && c < p.N) ? *(const uint32_t*)((const bf16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
+        }
+      }
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int c = col0 + ni * 16 + ((lane & 15) & ~1);
+    float2 lr[LATE ? 8 : 1][2], lc[LATE ? 8 : 1][2];
+    if constexpr (LATE) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int o = om[mi][t];
+          const bool ok = o >= 0 && c < p.N;
+          lr[mi][t] = (Rb && ok) ? ld_pair(Rb, remap(o, p.r_blk, p.r_rep) * p.ldr + c, p.r_f32) : make_float2(0.f, 0.f);
+          lc[mi][t] = (p.beta != 0.0f && ok) ? ld_pair(Cb, (long long)o * p.ldc + c, p.c_f32) : make_float2(0.f, 0.f);
+        }
+    }
+    const float bsw = dpp_swap1(bv[ni]);
+    const float b_lo = odd ? bsw : bv[ni], b_hi = odd ? bv[ni] : bsw;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float v0 = acc[mi][ni][2 * t] * p.alpha, v1 = acc[mi][ni][2 * t + 1] * p.alpha;
+        const float send = odd ? v0 : v1;
+        const float recv = dpp_swap1(send);
+        float lo = odd ? recv : v0, hi = odd ? v1 : recv;
+        if constexpr (LATE) {
+          lo += p.beta * lc[mi][t].x;
+          hi += p.beta * lc[mi][t].y;
+        }
+        lo += b_lo;
+        hi += b_hi;
+        const int o = om[mi][t];
+        const bool ok = o >= 0 && c < p.N;
+        const long long ci = (long long)o * p.ldc + c;
+        if (Pb && ok) st_pair(Pb, ci, p.pre_f32, lo, hi);
+        if (p.act == OCTSAM_ACT_RELU) {
+          lo = fmaxf(lo, 0.0f);
+          hi = fmaxf(hi, 0.0f);
+        } else if (p.act == OCTSAM_ACT_GELU) {
+          lo = gelu_erf(lo);
+          hi = gelu_erf(hi);
+        }
+        if (Rb) {
+          if constexpr (LATE) {
+            lo += lr[mi][t].x;
+            hi += lr[mi][t].y;
+          } else {
+            const uint32_t r = rv[LATE ? 0 : mi][LATE ? 0 : ni][t];
+            lo += __builtin_bit_cast(float, r << 16);
+            hi += __builtin_bit_cast(float, r & 0xffff0000u);
+          }
+        }
+        if (ok) st_pair(Cb, ci, p.c_f32, lo, hi);
+      }
+  }
+}
+
+// LDS-staged epilogue: the fp32 tile goes through LDS in two 128-row passes ([128][256+4] fp32,
+// padded against bank conflicts) and every lane then finishes 8 consecutive columns of one row with
+// 16-B vector loads (bias, residual, beta*C) and 16-B (bf16) / 2x16-B (fp32) stores: full cache lines
+// instead of the MFMA layout's 32-B row segments. Requires N, ldc (ldr) % 8 == 0 and 16-B aligned
+// C / C_pre / R (host-checked).
+constexpr int EPI_LD = 260;
+constexpr int EPI_BYTES = 128 * EPI_LD * 4;
+
+__device__ __forceinline__ void load8(const void* base, long long idx, bool f32, float (&v)[8]) {
+  if (f32) {
+    const float4 a = *(const float4*)((const float*)base + idx), b = *(const float4*)((const float*)base + idx + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    const bf16x8 a = *(const bf16x8*)((const bf16*)base + idx);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)a[e];
+  }
+}
+__device__ __forceinline__ void store8(void* base, long long idx, bool f32, const float (&v)[8]) {
+  if (f32) {
+    *(float4*)((float*)base + idx) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)base + idx + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    bf16x8 a;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = (bf16)v[e];
+    *(bf16x8*)((bf16*)base + idx) = a;
+  }
+}
+
+__device__ __forceinline__ void epilogue_lds(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0, int wr,
+                                             int wc, int wave, int lane, char* smem) {
+  float* st = (float*)smem;
+  char* Cb = (char*)p.C + bz * p.sC * (p.c_f32 ? 4 : 2);
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
+  const int c8 = (lane & 31) * 8;
+  const int n0 = col0 + c8;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = 0.0f;
+  if (p.bias && n0 < p.N) {
+    const float4 a = *(const float4*)(p.bias + n0), b = *(const float4*)(p.bias + n0 + 4);
+    bv[0] = a.x; bv[1] = a.y; bv[2] = a.z; bv[3] = a.w; bv[4] = b.x; bv[5] = b.y; bv[6] = b.z; bv[7] = b.w;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    raw_barrier();  // LDS free (main loop done / previous pass read)
+    if (wr == pass) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            st[(mi * 16 + 4 * (lane >> 4) + i) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][i];
+    }
+    raw_barrier();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rr = it * 16 + wave * 2 + (lane >> 5);
+      const int m = row0 + pass * 128 + rr;
+      if (m >= p.M || n0 >= p.N) continue;
+      const int om = p.row_map ? p.row_map[m] : m;
+      if (om < 0) continue;
+      const float4 a = *(const float4*)(st + rr * EPI_LD + c8), b = *(const float4*)(st + rr * EPI_LD + c8 + 4);
+      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const long long ci = (long long)om * p.ldc + n0;
+      float old[8], res[8];
+      if (p.beta != 0.0f) load8(Cb, ci, p.c_f32, old);
+      if (Rb) load8(Rb, remap(om, p.r_blk, p.r_rep) * p.ldr + n0, p.r_f32, res);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] *= p.alpha;
+        if (p.beta != 0.0f) v[e] += p.beta * old[e];
+        v[e] += bv[e];
+      }
+      if (Pb) store8(Pb, ci, p.pre_f32, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (p.act == OCTSAM_ACT_RELU) v[e] = fmaxf(v[e], 0.0f);
+        else if (p.act == OCTSAM_ACT_GELU) v[e] = gelu_erf(v[e]);
+        if (Rb) v[e] += res[e];
+      }
+      store8(Cb, ci, p.c_f32, v);
+    }
+  }
+}
+}  // namespace ph8
+
+#define PH8_MFMA_QUAD(MH, NH, BF)                                                                       \
+  __builtin_amdgcn_s_setprio(1);                                                                        \
+  _Pragma("unroll") for (int kb = 0; kb < 2; ++kb)                                                     \
+  _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                                     \
+  _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                                     \
+    acc[(MH) * 4 + mi][(NH) * 2 + ni] =                                                                 \
+        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+
+template <bool LATE>
+__global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = bid / per_batch, rem = bid - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 256;
+  const bf16* A = (const bf16*)p.A + bz * p.sA;
+  const bf16* B = (const bf16*)p.B + bz * p.sB;
+  const int nk = p.K / 64;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
+
+  // prologue: K-tile 0 (A-lo, B-n0 | B-n1 | A-hi), K-tile 1 (A-lo, B-n0 | B-n1)
+  ph8::load_region(p, A, B, 0, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region(p, A, B, 2, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region(p, A, B, 3, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region(p, A, B, 1, row0, col0, 0, gsm, wave, lane);
+  if (nk > 1) {
+    ph8::load_region(p, A, B, 0, row0, col0, 64, gsm + ph8::BUF, wave, lane);
+    ph8::load_region(p, A, B, 2, row0, col0, 64, gsm + ph8::BUF, wave, lane);
+    ph8::load_region(p, A, B, 3, row0, col0, 64, gsm + ph8::BUF, wave, lane);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    char* cur = gsm + (t & 1) * ph8::BUF;
+    char* nxt = gsm + ((t + 1) & 1) * ph8::BUF;
+    const char* ca = cur;
+    const char* cb = cur + 32768;
+    const bool h1 = t + 1 < nk, h2 = t + 2 < nk;
+    // ---- phase 0: Q(0,0) — A-lo, B-n0
+    if (h1) ph8::load_region(p, A, B, 1, row0, col0, (t + 1) * 64, nxt, wave, lane);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + mi * 16, kb * 4 + kq);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b0[ni][kb] = ph8::frag(cb, brow + ni * 16, kb * 4 + kq);
+    }
+    if (h1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // retire B-n1(t)
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(0, 0, b0)
+    raw_barrier();
+    // ---- phase 1: Q(0,1) — B-n1
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b1[ni][kb] = ph8::frag(cb, brow + 32 + ni * 16, kb * 4 + kq);
+    if (h1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // retire A-hi(t)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(0, 1, b1)
+    raw_barrier();
+    // ---- phase 2: Q(1,0) — A-hi; restage A-lo, B-n0 of K-tile t+2
+    if (h2) {
+      ph8::load_region(p, A, B, 0, row0, col0, (t + 2) * 64, cur, wave, lane);
+      ph8::load_region(p, A, B, 2, row0, col0, (t + 2) * 64, cur, wave, lane);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + 64 + mi * 16, kb * 4 + kq);
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(1, 0, b0)
+    raw_barrier();
+    // ---- phase 3: Q(1,1); restage B-n1 of K-tile t+2; retire A-lo, B-n0 of K-tile t+1
+    if (h2) ph8::load_region(p, A, B, 3, row0, col0, (t + 2) * 64, cur, wave, lane);
+    if (h2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (h1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    raw_barrier();
+    PH8_MFMA_QUAD(1, 1, b1)
+    raw_barrier();
+  }
+  if (wr == 0) raw_barrier();  // balance the stagger
+  ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
+}
+
+template <bool LATE>
+int launch_gemm8(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + 255) / 256;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8_kernel<LATE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ph8::EPI_BYTES);
+    attr = true;
+  }
+  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
+  hipLaunchKernelGGL((gemm8_kernel<LATE>), dim3((unsigned)nwg), dim3(512), ph8::EPI_BYTES, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
 }
 
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
@@ -739,6 +1095,16 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
     if (g_use_glds == 2) return launch_glds<128, 64, 3>(k, a, s);
     if (g_use_glds == 3) return launch_glds<256, 32, 4>(k, a, s);
     if (a->N <= 64) return launch_glds<64, 64, 3>(k, a, s);  // narrow outputs (ConvT 64-channel GEMMs)
+    // 8-phase kernel with the LDS-staged epilogue: 16-B aligned rows for every epilogue operand
+    const bool a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; }(a->C);
+    const bool epi8 = (a->N & 7) == 0 && (a->ldc & 7) == 0 && a16 && ((uintptr_t)a->bias & 15) == 0 &&
+                      ((uintptr_t)a->C_pre & 15) == 0 && ((uintptr_t)a->R & 15) == 0 &&
+                      (!a->R || (a->ldr & 7) == 0) && (a->batch == 1 || ((a->stride_c & 7) == 0 &&
+                                                                          (!a->R || (a->stride_r & 7) == 0)));
+    if (epi8 && g_use_glds != 5) {
+      t_last_path = 2;
+      return launch_gemm8<false>(k, a, s);
+    }
     return launch_glds<256, 64, 2>(k, a, s);
   }
   t_last_path = 0;

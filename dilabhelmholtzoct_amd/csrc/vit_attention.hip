@@ -230,6 +230,200 @@ __global__ __launch_bounds__(G_THR) void vit_attn_global_kernel(const bf16* __re
     }
 }
 
+// ------------------------------------------------------------------------------------ global, v2
+// 8 waves (256 queries = 4 image rows) per workgroup, two waves per SIMD so one wave's softmax overlaps
+// the other's MFMAs. K and V tiles (64 keys x 64 d) stream global -> LDS with global_load_lds into a
+// 3-deep ring (one instruction per wave per operand per tile, counted vmcnt + raw barrier). K keeps the
+// ds_read_b128 swizzle; V stays row-major and is read transposed with ds_read_b64_tr_b16 (its image
+// swaps 64-B halves on rows 2,3 mod 4 so the transposed reads are conflict-free). rel_w lives in
+// registers; rel_h as a [64 kh][32 q] fp32 table per wave. Softmax in base 2 (one FMA + exp per score).
+namespace g2 {
+constexpr int NW = 8, THR = NW * 64, NBUF = 3;
+constexpr int RELH_BYTES = NW * 64 * 32 * 4;       // 64 KiB
+constexpr int TILE_BYTES = 2 * 64 * 128;            // K + V, 16 KiB
+constexpr int SMEM = RELH_BYTES + NBUF * TILE_BYTES;  // 112 KiB
+constexpr int SCR_LD = 33;                          // rel_w scratch [96][33] per wave (overlaps the above)
+constexpr float L2E = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int vsw(int r, int c) { return r * 128 + ((c ^ (((r >> 1) & 1) << 2)) << 4); }
+__device__ __forceinline__ int ksw_b(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 32 table rows j0 .. j0+31 of P^T = R · Qs^T (times 8: undo the 1/8 folded into Qs), rows >= nrows zero.
+__device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows, const bf16x8 (&qf)[4],
+                                            int lane) {
+  const int h = lane >> 5, j = j0 + (lane & 31);
+  f32x16 acc = (f32x16)0.0f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bf16x8 a;
+    if (j >= 0 && j < nrows) {
+      const float* rp = R + j * 64 + 16 * s + 8 * h;
+      float4 x0 = *(const float4*)rp, x1 = *(const float4*)(rp + 4);
+      a[0] = (bf16)x0.x; a[1] = (bf16)x0.y; a[2] = (bf16)x0.z; a[3] = (bf16)x0.w;
+      a[4] = (bf16)x1.x; a[5] = (bf16)x1.y; a[6] = (bf16)x1.z; a[7] = (bf16)x1.w;
+    } else {
+      a = (bf16x8)(bf16)0.0f;
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
+  }
+  return acc * 8.0f;
+}
+
+// K and V tile `tile` -> ring slot: 8 instructions of 1 KiB (8 rows x 128 B) per operand, one per wave
+__device__ __forceinline__ void load_tile(const bf16* kbase, const bf16* vbase, int ld, int tile, char* slot,
+                                          int wave, int lane) {
+  const int r = wave * 8 + (lane >> 3), sl = lane & 7;
+  const long long row = (long long)(tile * 64 + r) * ld;
+  const int ck = sl ^ ((r >> 1) & 7), cv = sl ^ (((r >> 1) & 1) << 2);
+  __builtin_amdgcn_global_load_lds((const void*)(kbase + row + ck * 8), (lds_ptr_t)(slot + wave * 1024), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((const void*)(vbase + row + cv * 8), (lds_ptr_t)(slot + 8192 + wave * 1024), 16,
+                                   0, 0);
+}
+}  // namespace g2
+
+__global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16* __restrict__ qkv,
+                                                                      bf16* __restrict__ out,
+                                                                      const float* __restrict__ Rh,
+                                                                      const float* __restrict__ Rw, int heads) {
+  using namespace g2;
+  constexpr int S = 64, T = 4096, NT = T / 64;
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int head = blockIdx.y, seq = blockIdx.z;
+  const int D = heads * 64, ld = 3 * D;
+  const bf16* base = qkv + (long long)seq * T * ld;
+  const int q = blockIdx.x * (NW * 32) + wave * 32 + l32;
+  const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h));
+
+  // rel_w (registers): rows j = qw - kw + 63 in [qw0, qw0 + 95) of the table, staged through scratch
+  float* scr = (float*)gsm + wave * (96 * SCR_LD);
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 t = rel_block(Rw, qw0 + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * SCR_LD + l32] = t[r];
+  }
+  __syncthreads();
+  float relw[2][16];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * SCR_LD + l32] * L2E;
+  __syncthreads();
+  // rel_h table [kh][q]: row j = qh - kh + 63 -> block rows i = j - qh = 63 - kh
+  float* relh = (float*)gsm + wave * (64 * 32);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const f32x16 t = rel_block(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
+  }
+  __syncthreads();
+
+  const bf16* kbase = base + D + head * 64;
+  const bf16* vbase = base + 2 * D + head * 64;
+  char* ring = gsm + RELH_BYTES;
+  load_tile(kbase, vbase, ld, 0, ring, wave, lane);
+  load_tile(kbase, vbase, ld, 1, ring + TILE_BYTES, wave, lane);
+
+  f32x16 acc_o[2];
+  acc_o[0] = (f32x16)0.0f;
+  acc_o[1] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;  // base-2 running max / sum
+  // tr-read lane geometry (V^T operand): group g = lane >> 4, lane 4qq + pp of the group
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+
+  for (int tile = 0; tile < NT; ++tile) {
+    if (tile + 1 < NT) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (tile + 2 < NT) load_tile(kbase, vbase, ld, tile + 2, ring + ((tile + 2) % NBUF) * TILE_BYTES, wave, lane);
+    const char* sk = ring + (tile % NBUF) * TILE_BYTES;
+    const char* sv = sk + 8192;
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      sacc[t2] = (f32x16)0.0f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = *(const bf16x8*)(sk + ksw_b(t2 * 32 + l32, 2 * s + h));
+        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
+      }
+    }
+    const float rh = relh[tile * 32 + l32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = fmaf(sacc[t2][r], L2E, relw[t2][r] + rh);
+        sacc[t2][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.0f;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = __builtin_amdgcn_exp2f(sacc[t2][r] - m_new);
+        sacc[t2][r] = pv;
+        ls += pv;
+      }
+    l_run = fmaf(l_run, alpha, ls);
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
+#pragma unroll
+      for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
+    }
+    // O^T += V^T · P^T: P^T k-slot j of lane half hh is key 16ks + 8(j>>2) + 4hh + (j&3)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int td = 0; td < 2; ++td) {
+        const int r0 = 16 * ks + 4 * (g >> 1) + qq;
+        const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
+        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
+        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);
+      }
+    }
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  bf16* orow = out + ((long long)seq * T + q) * D + head * 64;
+#pragma unroll
+  for (int td = 0; td < 2; ++td)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * gg + e] * inv);
+      *(bf16x4*)(orow + td * 32 + 8 * gg + 4 * h) = o;
+    }
+}
+
 // ------------------------------------------------------------------------------------ window
 constexpr int W_NW = 7, W_THR = W_NW * 64;
 constexpr int W_KEYS = 256;
@@ -364,13 +558,26 @@ __global__ __launch_bounds__(W_THR) void vit_attn_window_kernel(const bf16* __re
 
 }  // namespace
 
+static int g_attn_v2 = 1;
+extern "C" void octsam_attention_set_variant(int32_t v) { g_attn_v2 = v; }
+
 extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w,
                                     int32_t nseq, int32_t side, int32_t heads, int32_t head_dim, void* stream) {
   OCTSAM_CHECK_ARG(qkv && out && rel_pos_h && rel_pos_w && nseq > 0 && heads > 0,
                    "octsam_vit_attention: bad args");
   OCTSAM_CHECK_ARG(head_dim == 64, "octsam_vit_attention: head_dim must be 64 (got %d)", head_dim);
   hipStream_t s = (hipStream_t)stream;
-  if (side == 64) {
+  if (side == 64 && g_attn_v2) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)vit_attn_global2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                g2::SMEM);
+      attr = true;
+    }
+    dim3 grid(4096 / (g2::NW * 32), heads, nseq);
+    hipLaunchKernelGGL(vit_attn_global2_kernel, grid, dim3(g2::THR), g2::SMEM, s, (const bf16*)qkv, (bf16*)out,
+                       rel_pos_h, rel_pos_w, heads);
+  } else if (side == 64) {
     dim3 grid(4096 / (G_NW * 32), heads, nseq);
     hipLaunchKernelGGL(vit_attn_global_kernel, grid, dim3(G_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
                        rel_pos_w, heads);

@@ -124,6 +124,9 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
  * out: bf16 [nseq, side*side, heads*64]; rel_pos_h/w: fp32 [2*side-1, 64].
  * side = 64 (global layers, nseq = batch) or 14 (windowed layers, nseq = batch * 25 windows).
  * softmax(q k^T / 8 + rel_h + rel_w) v with fp32 statistics; the T x T bias is never materialised. */
+/* select the global-attention kernel: 1 (default) = 8-wave LDS-DMA kernel with transposed V reads,
+   0 = 4-wave register-staged kernel (A/B testing) */
+void octsam_attention_set_variant(int32_t v);
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
                          int32_t side, int32_t heads, int32_t head_dim, void* stream);
 
