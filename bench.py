@@ -49,10 +49,14 @@ def parse():
     return p.parse_args()
 
 
+DOMINANT = "gemm8_kernel<false> (8-phase 256x256 bf16 NT GEMM: encoder QKV/proj/MLP, neck, decoder projections)"
+
+
 class GemmEventTimer:
-    """Wraps kernels.gemm: HIP events around every launch of the dominant kernel
-    (gemm_kernel<0,0>, the NT bf16 GEMM: all encoder Linear layers + decoder projections) on the stream
-    it is launched on; accumulates algorithmic FLOPs (2*M*N*K*batch)."""
+    """Wraps kernels.gemm: HIP events on the launch stream (torch's current stream, which every wrapper
+    passes to the library) around every GEMM launch in the timed region; octsam_gemm_last_path() tells
+    which kernel ran, and only the dominant one (path 2 = gemm8_kernel) is kept. Accumulates algorithmic
+    FLOPs 2*M*N*K*batch of those launches."""
 
     def __init__(self):
         from dilabhelmholtzoct_amd import kernels
@@ -65,15 +69,19 @@ class GemmEventTimer:
     def __enter__(self):
         orig = self.orig
 
+        from dilabhelmholtzoct_amd import _lib
+        lib = _lib.load()
+
         def wrapped(A, B, **kw):
-            if self.active and kw.get("a_mode", 0) == 0 and kw.get("b_mode", 0) == 0:
+            if self.active:
                 s = torch.cuda.Event(enable_timing=True)
                 e = torch.cuda.Event(enable_timing=True)
                 s.record()
                 out = orig(A, B, **kw)
                 e.record()
-                self.events.append((s, e))
-                self.flops += 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
+                if lib.octsam_gemm_last_path() == 2:
+                    self.events.append((s, e))
+                    self.flops += 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
                 return out
             return orig(A, B, **kw)
 
@@ -198,7 +206,7 @@ def main():
         ms, n, flops = timer.result()
         if n:
             achieved = flops / (ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": "gemm_kernel<0,0> (bf16 NT GEMM, all launches in the timed region)",
+            roof = {"bound": "mfma", "kernel": DOMINANT,
                     "achieved": round(achieved, 2), "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / MI355X_BF16_DENSE_TFLOPS, 4), "traffic": None,
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),

@@ -2,7 +2,7 @@
 # GPU-box check used each round: smoke, pytest -m gpu, bench, rocprofv3 kernel stats (outputs under gpurun_out/r01).
 set -u
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r01
+O=$R/gpurun_out/${TAG:-r01}
 mkdir -p $O
 cd $R
 timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
@@ -15,6 +15,6 @@ timeout -k 10 400 python bench.py > $O/bench.log 2>&1; rc=$?
 echo "bench rc=$rc"; tail -2 $O/bench.log
 [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline 0 --val 0 > $O/prof.log 2>&1; rc=$?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --cpu-baseline 0 --val 0 > $O/prof.log 2>&1; rc=$?
 echo "prof rc=$rc"
 exit $rc
