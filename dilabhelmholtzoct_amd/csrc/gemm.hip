@@ -870,19 +870,155 @@ __device__ __forceinline__ void epilogue_lds(const GemmK& p, f32x4 (&acc)[8][4],
     }
   }
 }
+
+// Register epilogue for the operand-swapped MFMA: acc[mi][ni] holds the 16x16 block transposed, so lane
+// (q = lane>>4, r = lane&15) owns output row m = 16*mi + r and the 4 consecutive columns 16*ni + 4q .. +3.
+// One v_permlane16_swap per value between blocks (2p, 2p+1) gives every lane 8 consecutive columns of its
+// row, starting at 32p + 16*(q&1) + 8*(q>>1): 16-B bf16 (32-B fp32) stores, 64-B row runs per
+// instruction, no LDS round trip and no barrier (the next tile's loads can be in flight). Every input the
+// stores depend on (row map, bias, residual, beta*C) is loaded before the first store, so no load waits
+// behind a store (vmcnt counts both). Requires N, ldc (ldr) % 8 == 0 and 16-B aligned C / C_pre / R / bias.
+template <int ACT>
+__device__ __forceinline__ float act_apply(float v) {
+  if constexpr (ACT == OCTSAM_ACT_RELU) return fmaxf(v, 0.0f);
+  else if constexpr (ACT == OCTSAM_ACT_GELU) return gelu_fast(v);
+  else return v;
+}
+
+template <int ACT>
+__device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0,
+                                             int lane) {
+  char* Cb = (char*)p.C + bz * p.sC * (p.c_f32 ? 4 : 2);
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
+  const int q = lane >> 4;
+  const int cofs = 16 * (q & 1) + 8 * (q >> 1);
+  // permute first (all lanes active), then everything is per-lane elementwise on 8 consecutive columns
+  float v[8][2][8];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      // (bit-cast the whole vector first: hipcc 7.2 drops all but element 0 of a per-element
+      // __builtin_bit_cast(uint32_t, f32x4[i]) feeding this builtin)
+      const u32x4 x = __builtin_bit_cast(u32x4, acc[mi][2 * pr]), y = __builtin_bit_cast(u32x4, acc[mi][2 * pr + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t xi = x[i], yi = y[i];
+        const auto r = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
+        v[mi][pr][i] = __builtin_bit_cast(float, (uint32_t)r[0]);
+        v[mi][pr][4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
+      }
+    }
+  int om[8];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = row0 + 16 * mi + (lane & 15);
+    om[mi] = m < p.M ? (p.row_map ? p.row_map[m] : m) : -1;
+  }
+  float bv[2][8];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const int n = col0 + 32 * pr + cofs;
+    if (p.bias && n < p.N) {
+      const float4 a = *(const float4*)(p.bias + n), b = *(const float4*)(p.bias + n + 4);
+      bv[pr][0] = a.x; bv[pr][1] = a.y; bv[pr][2] = a.z; bv[pr][3] = a.w;
+      bv[pr][4] = b.x; bv[pr][5] = b.y; bv[pr][6] = b.z; bv[pr][7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[pr][e] = 0.0f;
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[mi][pr][e] = v[mi][pr][e] * p.alpha + bv[pr][e];
+  // (beta != 0 is routed to the other kernels by the host)
+  auto finish = [&](int mi, int pr, const float (&res)[8]) {
+    const int n = col0 + 32 * pr + cofs;
+    const bool ok = om[mi] >= 0 && n < p.N;
+    const long long ci = (long long)om[mi] * p.ldc + n;
+    if (Pb && ok) store8(Pb, ci, p.pre_f32, v[mi][pr]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[mi][pr][e] = act_apply<ACT>(v[mi][pr][e]) + res[e];
+    if (ok) store8(Cb, ci, p.c_f32, v[mi][pr]);
+  };
+  if (Rb && !p.r_f32) {
+    u32x4 raw[8][2];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int n = col0 + 32 * pr + cofs;
+        raw[mi][pr] = (om[mi] >= 0 && n < p.N)
+                          ? *(const u32x4*)((const bf16*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n)
+                          : (u32x4)0u;
+      }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        float res[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          res[2 * e] = __builtin_bit_cast(float, raw[mi][pr][e] << 16);
+          res[2 * e + 1] = __builtin_bit_cast(float, raw[mi][pr][e] & 0xffff0000u);
+        }
+        finish(mi, pr, res);
+      }
+  } else if (Rb) {  // fp32 residual: two halves of 4 row blocks (register budget)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 raw[4][2][2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int mi = 4 * h + j, n = col0 + 32 * pr + cofs;
+          if (om[mi] >= 0 && n < p.N) {
+            const float* s = (const float*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n;
+            raw[j][pr][0] = *(const float4*)s;
+            raw[j][pr][1] = *(const float4*)(s + 4);
+          } else {
+            raw[j][pr][0] = raw[j][pr][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const float res[8] = {raw[j][pr][0].x, raw[j][pr][0].y, raw[j][pr][0].z, raw[j][pr][0].w,
+                                raw[j][pr][1].x, raw[j][pr][1].y, raw[j][pr][1].z, raw[j][pr][1].w};
+          finish(4 * h + j, pr, res);
+        }
+    }
+  } else {
+    const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) finish(mi, pr, zero);
+  }
+}
 }  // namespace ph8
 
+// TR (register epilogue): operands swapped, the accumulator holds each 16x16 block transposed
 #define PH8_MFMA_QUAD(MH, NH, BF)                                                                       \
   __builtin_amdgcn_s_setprio(1);                                                                        \
   _Pragma("unroll") for (int kb = 0; kb < 2; ++kb)                                                     \
   _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                                     \
   _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                                     \
     acc[(MH) * 4 + mi][(NH) * 2 + ni] =                                                                 \
-        __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
+        TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[ni][kb], af[mi][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0) \
+           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
 
-template <int DBG>
+// EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA)
+template <int DBG, int EPI>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
+  constexpr bool TR = EPI >= 0;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -987,22 +1123,23 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     if (x == 12345.f) ((float*)p.C)[0] = x;
     return;
   }
-  ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
+  if constexpr (TR) ph8::epilogue_reg<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+  else ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
 }
 
-template <int DBG>
+template <int DBG, int EPI>
 int launch_gemm8(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + 255) / 256;
+  constexpr int LDS = EPI < 0 ? ph8::EPI_BYTES : 2 * ph8::BUF;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8_kernel<DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              ph8::EPI_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm8_kernel<DBG, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
   const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
-  hipLaunchKernelGGL((gemm8_kernel<DBG>), dim3((unsigned)nwg), dim3(512), ph8::EPI_BYTES, s, g);
+  hipLaunchKernelGGL((gemm8_kernel<DBG, EPI>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
 }
@@ -1111,11 +1248,14 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
                       ((uintptr_t)a->C_pre & 15) == 0 && ((uintptr_t)a->R & 15) == 0 &&
                       (!a->R || (a->ldr & 7) == 0) && (a->batch == 1 || ((a->stride_c & 7) == 0 &&
                                                                           (!a->R || (a->stride_r & 7) == 0)));
-    if (epi8 && g_use_glds != 5) {
+    if (epi8 && g_use_glds != 5 && a->beta == 0.0f) {
       t_last_path = 2;
-      if (g_use_glds == 6) return launch_gemm8<1>(k, a, s);
-      if (g_use_glds == 7) return launch_gemm8<2>(k, a, s);
-      return launch_gemm8<0>(k, a, s);
+      if (g_use_glds == 6) return launch_gemm8<1, 0>(k, a, s);
+      if (g_use_glds == 7) return launch_gemm8<2, 0>(k, a, s);
+      if (g_use_glds == 8) return launch_gemm8<0, -1>(k, a, s);
+      if (a->act == OCTSAM_ACT_RELU) return launch_gemm8<0, OCTSAM_ACT_RELU>(k, a, s);
+      if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<0, OCTSAM_ACT_GELU>(k, a, s);
+      return launch_gemm8<0, 0>(k, a, s);
     }
     return launch_glds<256, 64, 2>(k, a, s);
   }

@@ -1,4 +1,4 @@
-// LayerNorm over the last dimension (one wave per row), forward and backward.
+// LayerNorm over the last dimension, forward and backward.
 //
 // Covers nn.LayerNorm of SamVisionLayer (hf:modeling_sam.py:954-972, eps 1e-6), the channels-first
 // SamLayerNorm of the neck and of the mask-decoder upscaling (:975-992, :519-521; applied per pixel on
@@ -8,82 +8,150 @@
 // writes zeros when src_rows[r] < 0); mean/rstd saved for backward.
 // Backward: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w (optionally through the
 // fused GELU); per-block dw/db partials reduced deterministically by octsam_splitk_reduce.
+//
+// Layout: a row is owned by a group of G lanes (G = 8 for D = 64, 32 for D = 256, 64 otherwise), so a
+// wave holds 64/G rows; lane j of a group owns NCH chunks of CW consecutive columns at CW*j + G*CW*c
+// (16-B bf16 / 32-B fp32 vector accesses, whole cache lines per wave instruction). Grid-stride over
+// row groups; the statistics reduce with xor-shuffles inside the group.
 #include "common.h"
 #include "../../include/octsam.h"
 
 namespace {
 
-template <typename T>
-__device__ __forceinline__ float ld(const T* p, long long i) { return (float)p[i]; }
+template <int D>
+struct LnGeo;
+template <> struct LnGeo<64> { static constexpr int G = 8, CW = 8, NCH = 1; };
+template <> struct LnGeo<256> { static constexpr int G = 32, CW = 8, NCH = 1; };
+template <> struct LnGeo<768> { static constexpr int G = 64, CW = 4, NCH = 3; };
+template <> struct LnGeo<1024> { static constexpr int G = 64, CW = 8, NCH = 2; };
+template <> struct LnGeo<1280> { static constexpr int G = 64, CW = 4, NCH = 5; };
 
-template <int PL>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_f32, const int* __restrict__ src_rows,
-                                                     long long rows, const float* __restrict__ w,
-                                                     const float* __restrict__ b, float eps, void* __restrict__ y,
-                                                     int y_f32, void* __restrict__ y2, int act,
-                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  constexpr int D = PL * 64;
-  const int lane = threadIdx.x & 63;
-  long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  long long src = src_rows ? (long long)src_rows[row] : row;
-  float v[PL];
-  if (src < 0) {
-#pragma unroll
-    for (int i = 0; i < PL; ++i) v[i] = 0.0f;
-  } else if (x_f32) {
-    const float* xr = (const float*)x + src * D;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) v[i] = xr[i * 64 + lane];
-  } else {
-    const bf16* xr = (const bf16*)x + src * D;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) v[i] = (float)xr[i * 64 + lane];
-  }
-  float out[PL];
-  if (src < 0) {
-    // window padding: HF pads AFTER layer_norm1, so padded tokens are exact zeros
-#pragma unroll
-    for (int i = 0; i < PL; ++i) out[i] = 0.0f;
-    if (mean_out) { if (lane == 0) { mean_out[row] = 0.0f; rstd_out[row] = 0.0f; } }
-  } else {
-    float s = 0.0f;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) s += v[i];
-    const float mean = wave_sum(s) * (1.0f / D);
-    float q = 0.0f;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) { float d = v[i] - mean; q += d * d; }
-    const float var = wave_sum(q) * (1.0f / D);
-    const float rstd = rsqrtf(var + eps);
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      int c = i * 64 + lane;
-      float o = (v[i] - mean) * rstd * w[c] + b[c];
-      if (act == OCTSAM_ACT_GELU) o = gelu_erf(o);
-      else if (act == OCTSAM_ACT_RELU) o = fmaxf(o, 0.0f);
-      out[i] = o;
+template <int CW>
+__device__ __forceinline__ void ldv(const void* base, long long idx, bool f32, float* v) {
+  if (f32) {
+    const float* p = (const float*)base + idx;
+    if constexpr (CW == 8) {
+      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      const float4 a = *(const float4*)p;
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     }
-    if (mean_out && lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
-  }
-  if (y_f32) {
-    float* yr = (float*)y + row * D;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) yr[i * 64 + lane] = out[i];
   } else {
-    bf16* yr = (bf16*)y + row * D;
+    const bf16* p = (const bf16*)base + idx;
+    if constexpr (CW == 8) {
+      const u32x4 a = *(const u32x4*)p;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) yr[i * 64 + lane] = (bf16)out[i];
-  }
-  if (y2) {  // secondary fp32 copy (residual stream)
-    float* yr = (float*)y2 + row * D;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) yr[i * 64 + lane] = out[i];
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = __builtin_bit_cast(float, a[e] << 16);
+        v[2 * e + 1] = __builtin_bit_cast(float, a[e] & 0xffff0000u);
+      }
+    } else {
+      const uint2 a = *(const uint2*)p;
+      v[0] = __builtin_bit_cast(float, a.x << 16);
+      v[1] = __builtin_bit_cast(float, a.x & 0xffff0000u);
+      v[2] = __builtin_bit_cast(float, a.y << 16);
+      v[3] = __builtin_bit_cast(float, a.y & 0xffff0000u);
+    }
   }
 }
 
-// Backward. grid-stride over rows; each block keeps dw/db partials for its rows.
-template <int PL>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16x2 w;
+  w[0] = (bf16)a;
+  w[1] = (bf16)b;
+  return __builtin_bit_cast(uint32_t, w);
+}
+
+template <int CW>
+__device__ __forceinline__ void stv(void* base, long long idx, bool f32, const float* v) {
+  if (f32) {
+    float* p = (float*)base + idx;
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    if constexpr (CW == 8) *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    bf16* p = (bf16*)base + idx;
+    if constexpr (CW == 8) {
+      u32x4 a;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = pack2(v[2 * e], v[2 * e + 1]);
+      *(u32x4*)p = a;
+    } else {
+      *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+}
+
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_f32, const int* __restrict__ src_rows,
+                                                     long long rows, const float* __restrict__ w,
+                                                     const float* __restrict__ b, float eps, void* __restrict__ y,
+                                                     int y_f32, float* __restrict__ y2, int act,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  using Geo = LnGeo<D>;
+  constexpr int G = Geo::G, CW = Geo::CW, NCH = Geo::NCH, RPW = 64 / G, PL = CW * NCH;
+  const int lane = threadIdx.x & 63, j = lane % G;
+  float wv[PL], bv[PL];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    ldv<CW>(w, CW * j + G * CW * c, true, wv + c * CW);
+    ldv<CW>(b, CW * j + G * CW * c, true, bv + c * CW);
+  }
+  const long long nwaves = (long long)gridDim.x * 4;
+  for (long long rg = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); rg * RPW < rows; rg += nwaves) {
+    const long long row = rg * RPW + lane / G;
+    const bool live = row < rows;
+    const long long src = !live ? -1 : (src_rows ? (long long)src_rows[row] : row);
+    float v[PL];
+    if (src >= 0) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) ldv<CW>(x, src * D + CW * j + G * CW * c, x_f32, v + c * CW);
+    } else {
+#pragma unroll
+      for (int e = 0; e < PL; ++e) v[e] = 0.0f;
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int e = 0; e < PL; ++e) s += v[e];
+    const float mean = group_sum<G>(s) * (1.0f / D);
+    float q = 0.0f;
+#pragma unroll
+    for (int e = 0; e < PL; ++e) {
+      const float d = v[e] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(group_sum<G>(q) * (1.0f / D) + eps);
+    if (!live) continue;
+    float out[PL];
+#pragma unroll
+    for (int e = 0; e < PL; ++e) {
+      float o = (v[e] - mean) * rstd * wv[e] + bv[e];
+      if (act == OCTSAM_ACT_GELU) o = gelu_fast(o);
+      else if (act == OCTSAM_ACT_RELU) o = fmaxf(o, 0.0f);
+      // window padding: HF pads AFTER layer_norm1, so padded tokens are exact zeros
+      out[e] = src >= 0 ? o : 0.0f;
+    }
+    if (mean_out && j == 0) {
+      mean_out[row] = src >= 0 ? mean : 0.0f;
+      rstd_out[row] = src >= 0 ? rstd : 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      stv<CW>(y, row * D + CW * j + G * CW * c, y_f32, out + c * CW);
+      if (y2) stv<CW>(y2, row * D + CW * j + G * CW * c, true, out + c * CW);  // fp32 residual-stream copy
+    }
+  }
+}
+
+// Backward. Grid-stride over row groups; each block writes one dw/db partial row (fixed order).
+template <int D>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, const void* __restrict__ x,
                                                      int x_f32, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ w,
@@ -91,84 +159,110 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
                                                      void* __restrict__ dx, int dx_f32, float beta,
                                                      bf16* __restrict__ dx2, float* __restrict__ dw_part,
                                                      float* __restrict__ db_part) {
-  constexpr int D = PL * 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float dwa[PL], dba[PL];
+  using Geo = LnGeo<D>;
+  constexpr int G = Geo::G, CW = Geo::CW, NCH = Geo::NCH, RPW = 64 / G, PL = CW * NCH;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane % G;
+  float wv[PL], bv[PL], dwa[PL], dba[PL];
 #pragma unroll
-  for (int i = 0; i < PL; ++i) { dwa[i] = 0.0f; dba[i] = 0.0f; }
-  for (long long row = (long long)blockIdx.x * 4 + wave; row < rows; row += (long long)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
+  for (int c = 0; c < NCH; ++c) {
+    ldv<CW>(w, CW * j + G * CW * c, true, wv + c * CW);
+    ldv<CW>(b, CW * j + G * CW * c, true, bv + c * CW);
+  }
+#pragma unroll
+  for (int e = 0; e < PL; ++e) { dwa[e] = 0.0f; dba[e] = 0.0f; }
+  const long long nwaves = (long long)gridDim.x * 4;
+  for (long long rg = (long long)blockIdx.x * 4 + wave; rg * RPW < rows; rg += nwaves) {
+    const long long row = rg * RPW + lane / G;
+    const bool live = row < rows;
+    const long long rr = live ? row : rows - 1;  // dead lanes compute on a valid row, contribute nothing
+    const float mu = mean[rr], rs = rstd[rr];
     float xh[PL], g[PL];
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      int c = i * 64 + lane;
-      float xv = x_f32 ? ((const float*)x)[row * D + c] : (float)((const bf16*)x)[row * D + c];
-      float gy = dy_f32 ? ((const float*)dy)[row * D + c] : (float)((const bf16*)dy)[row * D + c];
-      xh[i] = (xv - mu) * rs;
-      if (act == OCTSAM_ACT_GELU) {
-        float pre = xh[i] * w[c] + b[c];
-        gy *= gelu_erf_grad(pre);
-      } else if (act == OCTSAM_ACT_RELU) {
-        float pre = xh[i] * w[c] + b[c];
-        gy = pre > 0.0f ? gy : 0.0f;
-      }
-      dwa[i] += gy * xh[i];
-      dba[i] += gy;
-      g[i] = gy * w[c];
+    for (int c = 0; c < NCH; ++c) {
+      ldv<CW>(x, rr * D + CW * j + G * CW * c, x_f32, xh + c * CW);
+      ldv<CW>(dy, rr * D + CW * j + G * CW * c, dy_f32, g + c * CW);
     }
     float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) { s1 += g[i]; s2 += g[i] * xh[i]; }
-    s1 = wave_sum(s1) * (1.0f / D);
-    s2 = wave_sum(s2) * (1.0f / D);
+    for (int e = 0; e < PL; ++e) {
+      xh[e] = (xh[e] - mu) * rs;
+      float gy = live ? g[e] : 0.0f;
+      if (act == OCTSAM_ACT_GELU) gy *= gelu_fast_grad(xh[e] * wv[e] + bv[e]);
+      else if (act == OCTSAM_ACT_RELU) gy = xh[e] * wv[e] + bv[e] > 0.0f ? gy : 0.0f;
+      dwa[e] += gy * xh[e];
+      dba[e] += gy;
+      g[e] = gy * wv[e];
+      s1 += g[e];
+      s2 += g[e] * xh[e];
+    }
+    s1 = group_sum<G>(s1) * (1.0f / D);
+    s2 = group_sum<G>(s2) * (1.0f / D);
+    if (!live) continue;
+    float d[PL];
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      int c = i * 64 + lane;
-      float d = rs * (g[i] - s1 - xh[i] * s2);
-      if (dx_f32) {
-        float* p = (float*)dx + row * D + c;
-        d = (beta != 0.0f ? beta * *p : 0.0f) + d;
-        *p = d;
-      } else {
-        bf16* p = (bf16*)dx + row * D + c;
-        d = (beta != 0.0f ? beta * (float)*p : 0.0f) + d;
-        *p = (bf16)d;
+    for (int e = 0; e < PL; ++e) d[e] = rs * (g[e] - s1 - xh[e] * s2);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const long long idx = row * D + CW * j + G * CW * c;
+      if (beta != 0.0f) {
+        float old[CW];
+        ldv<CW>(dx, idx, dx_f32, old);
+#pragma unroll
+        for (int e = 0; e < CW; ++e) d[c * CW + e] += beta * old[e];
       }
-      if (dx2) dx2[row * D + c] = (bf16)d;
+      stv<CW>(dx, idx, dx_f32, d + c * CW);
+      if (dx2) stv<CW>(dx2, idx, false, d + c * CW);
     }
   }
-  // block-level reduction of dw/db partials over the 4 waves through LDS
-  __shared__ float red[4][D];
+  // rows of one wave that share columns: fold the RPW groups, then the 4 waves through LDS
 #pragma unroll
-  for (int i = 0; i < PL; ++i) red[wave][i * 64 + lane] = dwa[i];
-  __syncthreads();
-  for (int c = threadIdx.x; c < D; c += 256) dw_part[(long long)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-  __syncthreads();
+  for (int e = 0; e < PL; ++e) {
 #pragma unroll
-  for (int i = 0; i < PL; ++i) red[wave][i * 64 + lane] = dba[i];
+    for (int o = G; o < 64; o <<= 1) {
+      dwa[e] += __shfl_xor(dwa[e], o, 64);
+      dba[e] += __shfl_xor(dba[e], o, 64);
+    }
+  }
+  __shared__ float red[2][4][D];
+  if (lane < G) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int e = 0; e < CW; ++e) {
+        red[0][wave][CW * j + G * CW * c + e] = dwa[c * CW + e];
+        red[1][wave][CW * j + G * CW * c + e] = dba[c * CW + e];
+      }
+  }
   __syncthreads();
-  for (int c = threadIdx.x; c < D; c += 256) db_part[(long long)blockIdx.x * D + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  for (int c = threadIdx.x; c < D; c += 256) {
+    dw_part[(long long)blockIdx.x * D + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    db_part[(long long)blockIdx.x * D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
 }
 
-template <int PL>
+template <int D>
 int fwd_launch(const void* x, int x_f32, const int* src_rows, long long rows, const float* w, const float* b, float eps,
-               void* y, int y_f32, void* y2, int act, float* mean, float* rstd, hipStream_t s) {
-  unsigned blocks = (unsigned)((rows + 3) / 4);
-  hipLaunchKernelGGL(ln_fwd_kernel<PL>, dim3(blocks), dim3(256), 0, s, x, x_f32, src_rows, rows, w, b, eps, y, y_f32,
+               void* y, int y_f32, float* y2, int act, float* mean, float* rstd, hipStream_t s) {
+  constexpr int RPB = 4 * (64 / LnGeo<D>::G);  // rows per block per grid-stride step
+  const long long need = (rows + RPB - 1) / RPB;
+  const unsigned blocks = (unsigned)(need < 8192 ? need : 8192);
+  hipLaunchKernelGGL(ln_fwd_kernel<D>, dim3(blocks), dim3(256), 0, s, x, x_f32, src_rows, rows, w, b, eps, y, y_f32,
                      y2, act, mean, rstd);
   OCTSAM_LAUNCH_CHECK("octsam_layernorm_fwd");
   return 0;
 }
 
-template <int PL>
+template <int D>
 int bwd_launch(const void* dy, int dy_f32, const void* x, int x_f32, const float* mean, const float* rstd,
                const float* w, const float* b, int act, long long rows, void* dx, int dx_f32, float beta,
                bf16* dx2, float* dw_part, float* db_part, int nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(ln_bwd_kernel<PL>, dim3(nblocks), dim3(256), 0, s, dy, dy_f32, x, x_f32, mean, rstd, w, b, act,
+  hipLaunchKernelGGL(ln_bwd_kernel<D>, dim3(nblocks), dim3(256), 0, s, dy, dy_f32, x, x_f32, mean, rstd, w, b, act,
                      rows, dx, dx_f32, beta, dx2, dw_part, db_part);
   OCTSAM_LAUNCH_CHECK("octsam_layernorm_bwd");
   return 0;
 }
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
@@ -177,13 +271,15 @@ extern "C" int octsam_layernorm_fwd(const void* x, int32_t x_f32, const int32_t*
                                     int32_t act, float* mean, float* rstd, void* stream) {
   OCTSAM_CHECK_ARG(x && w && b && y && rows > 0, "octsam_layernorm_fwd: bad args");
   OCTSAM_CHECK_ARG((mean == nullptr) == (rstd == nullptr), "octsam_layernorm_fwd: mean/rstd both or neither");
+  OCTSAM_CHECK_ARG(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(b) && (!y2_f32 || aligned16(y2_f32)),
+                   "octsam_layernorm_fwd: x, y, y2, w, b must be 16-B aligned");
   hipStream_t s = (hipStream_t)stream;
   switch (D) {
-    case 64: return fwd_launch<1>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
-    case 256: return fwd_launch<4>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
-    case 768: return fwd_launch<12>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
-    case 1024: return fwd_launch<16>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
-    case 1280: return fwd_launch<20>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
+    case 64: return fwd_launch<64>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
+    case 256: return fwd_launch<256>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
+    case 768: return fwd_launch<768>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
+    case 1024: return fwd_launch<1024>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
+    case 1280: return fwd_launch<1280>(x, x_f32, src_rows, rows, w, b, eps, y, y_f32, y2_f32, act, mean, rstd, s);
     default: octsam::set_error("octsam_layernorm_fwd: unsupported D=%d", D); return 1;
   }
 }
@@ -194,11 +290,15 @@ extern "C" int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* 
                                     float* db_part, int32_t nblocks, void* stream) {
   OCTSAM_CHECK_ARG(dy && x && mean && rstd && w && b && dx && dw_part && db_part && rows > 0 && nblocks > 0,
                    "octsam_layernorm_bwd: bad args");
+  OCTSAM_CHECK_ARG(aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(w) && aligned16(b) &&
+                       (!dx2_bf16 || aligned16(dx2_bf16)),
+                   "octsam_layernorm_bwd: dy, x, dx, dx2, w, b must be 16-B aligned");
   hipStream_t s = (hipStream_t)stream;
   switch (D) {
-    case 64: return bwd_launch<1>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
-    case 256: return bwd_launch<4>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
-    case 768: return bwd_launch<12>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 64: return bwd_launch<64>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 256: return bwd_launch<256>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 768: return bwd_launch<768>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
+    case 1024: return bwd_launch<1024>(dy, dy_f32, x, x_f32, mean, rstd, w, b, act, rows, dx, dx_f32, beta, (bf16*)dx2_bf16, dw_part, db_part, nblocks, s);
     default: octsam::set_error("octsam_layernorm_bwd: unsupported D=%d", D); return 1;
   }
 }

@@ -141,7 +141,9 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     rm[::7] = -1
     rm = rm.to(cuda)
     outs = []
-    for fast in (1, 5, 0):  # 1: 8-phase kernel (LDS-staged epilogue), 5: persistent ring kernel, 0: generic
+    # 1: 8-phase kernel (register epilogue; beta != 0 goes to the ring kernel), 8: 8-phase with the LDS-staged
+    # epilogue, 5: persistent ring kernel, 0: generic
+    for fast in (1, 8, 5, 0):
         lib.octsam_gemm_set_fast_path(fast)
         out = C0.clone()
         pout = None if pre is None else torch.zeros(Bt, M, N, device=cuda,
@@ -151,7 +153,8 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
         if R is not None:
             kw.update(residual=R, stride_r=M * N)
         kernels.gemm(A, W, **kw)
-        assert lib.octsam_gemm_last_path() == {1: 2, 5: 1, 0: 0}[fast]
+        p8 = 2 if beta == 0.0 else 1
+        assert lib.octsam_gemm_last_path() == {1: p8, 8: p8, 5: 1, 0: 0}[fast]
         outs.append((out, pout))
     lib.octsam_gemm_set_fast_path(1)
     keep = (rm >= 0).nonzero().flatten()
@@ -168,7 +171,27 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     drop[dst] = False
     for out, _ in outs:
         assert torch.equal(out[:, drop], C0[:, drop])
-    assert _rel(outs[0][0], outs[2][0]) < tol and _rel(outs[1][0], outs[2][0]) < tol
+    assert all(_rel(o[0], outs[-1][0]) < tol for o in outs[:-1])
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(4096, 2304, 768), (1100, 264, 128)])
+def test_gemm8_register_epilogue_act(cuda, act, M, N, K):
+    """8-phase kernel, register epilogue, each activation against torch fp32 (bf16 out, bf16 residual)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(act * 7 + M)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    lib.octsam_gemm_set_fast_path(1)
+    kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, act=act, residual=R)
+    assert lib.octsam_gemm_last_path() == 2
+    pre = A.float() @ W.float().t() + bias
+    ref = {0: pre, 1: F.relu(pre), 2: F.gelu(pre)}[act] + R.float()
+    assert _rel(out, ref) < 8e-3
 
 
 @pytest.mark.parametrize("a_mode,b_mode", [(1, 0), (0, 1), (1, 1)])

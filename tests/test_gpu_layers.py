@@ -40,6 +40,34 @@ def test_layernorm_fwd_bwd(cuda, D, act):
     assert _rel(db, br.grad) < 1e-4
 
 
+@pytest.mark.parametrize("D", [64, 256, 768])
+@pytest.mark.parametrize("rows", [37, 4099])
+def test_layernorm_bf16_beta_dual(cuda, D, rows):
+    """bf16 input / fp32 second output (decoder residual stream), ragged row counts; backward with bf16 dy,
+    beta-accumulated fp32 dx and the bf16 dx copy."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(D * 3 + rows)
+    x = (torch.randn(rows, D, generator=g) * 2 - 0.5).to(cuda, torch.bfloat16)
+    w = torch.randn(D, generator=g).to(cuda)
+    b = torch.randn(D, generator=g).to(cuda)
+    y = torch.empty(rows, D, device=cuda, dtype=torch.bfloat16)
+    y2 = torch.empty(rows, D, device=cuda)
+    mean = torch.empty(rows, device=cuda)
+    rstd = torch.empty(rows, device=cuda)
+    kernels.layernorm_fwd(x, w, b, 1e-6, y, out2_f32=y2, mean=mean, rstd=rstd)
+    xr = x.float().requires_grad_()
+    ref = F.layer_norm(xr, (D,), w, b, 1e-6)
+    assert _rel(y2, ref) < 1e-5 and _rel(y, ref) < 8e-3
+    dy = torch.randn(rows, D, generator=g).to(cuda, torch.bfloat16)
+    ref.backward(dy.float())
+    dx0 = torch.randn(rows, D, generator=g).to(cuda)
+    dx = dx0.clone()
+    dx2 = torch.empty(rows, D, device=cuda, dtype=torch.bfloat16)
+    kernels.layernorm_bwd(dy, x, mean, rstd, w, b, dx, beta=1.0, dx2_bf16=dx2)
+    want = xr.grad + dx0
+    assert _rel(dx, want) < 1e-4 and _rel(dx2, want) < 8e-3
+
+
 def test_layernorm_gather_rows(cuda):
     from dilabhelmholtzoct_amd import kernels
     x = torch.randn(10, 768, device=cuda)
