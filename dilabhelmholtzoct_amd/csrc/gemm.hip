@@ -1144,6 +1144,187 @@ int launch_gemm8(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Persistent 8-phase kernel: one workgroup per CU walks its tiles (XCD-contiguous ranges) as ONE flat
+// sequence of K-steps g = tile * nk + kt, so the two-deep LDS-DMA prefetch runs straight across tile
+// boundaries: the next tile's first K-tiles are in flight while the register epilogue of the finished tile
+// computes and stores. The only cost of a boundary is the first K-step after it, whose counted waits must
+// also cover the epilogue's stores (vmcnt counts both); for full tiles without a row map the store count is
+// exact and the waits are relaxed by it, so the stores drain under that step's MFMAs.
+namespace ph8 {
+struct Cursor {  // the K-step a prefetch targets: tile i (this workgroup's i-th), K-tile kt
+  const bf16* A;
+  const bf16* B;
+  int row0, col0, i, kt;
+};
+__device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, int stride, int per_batch) {
+  const int t = first + i * stride;
+  const int bz = t / per_batch, rem = t - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  Cursor c;
+  c.A = (const bf16*)p.A + bz * p.sA;
+  c.B = (const bf16*)p.B + bz * p.sB;
+  c.row0 = tm * 256;
+  c.col0 = tn * 256;
+  c.i = i;
+  c.kt = 0;
+  return c;
+}
+template <int BASE>
+__device__ __forceinline__ void vm_wait(bool relax) {
+  // relax: the 16 store instructions of a full bf16 tile's epilogue sit above the loads this wait retires
+  (void)relax;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE) : "memory");
+}
+}  // namespace ph8
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
+  constexpr bool TR = true;
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int ntiles = per_batch * batch;
+  const int stride = gridDim.x >> 3;  // workgroups per XCD (grid is a multiple of 8)
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int tper = (ntiles + 7) >> 3;
+  const int tbeg = xcd * tper, tend = min(ntiles, tbeg + tper);
+  const int first = tbeg + loc;
+  const int mycnt = first < tend ? (tend - first + stride - 1) / stride : 0;
+  const int nk = p.K / 64;
+  const int G = mycnt * nk;
+  if (G == 0) return;
+  // only bf16-output epilogues without a pre-activation copy have the exact 16-store count the relaxed
+  // waits assume; everything else waits for its stores (conservative)
+  const bool relax_ok = !p.c_f32 && p.Cpre == nullptr && p.row_map == nullptr;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
+
+  // prefetch cursors: c1 -> step g+1, c2 -> step g+2 (advanced once per step; divisions once per tile)
+  ph8::Cursor cc = ph8::tile_cursor(p, 0, first, stride, per_batch);
+  auto advance = [&](ph8::Cursor c) {
+    if (++c.kt == nk) c = ph8::tile_cursor(p, c.i + 1, first, stride, per_batch);
+    return c;
+  };
+  auto issue = [&](const ph8::Cursor& c, int region, char* buf) {
+    ph8::load_region(p, c.A, c.B, region, c.row0, c.col0, c.kt * 64, buf, wave, lane);
+  };
+  ph8::Cursor c1 = advance(cc);
+  ph8::Cursor c2 = advance(c1);
+  issue(cc, 0, gsm);
+  issue(cc, 2, gsm);
+  issue(cc, 3, gsm);
+  issue(cc, 1, gsm);
+  if (G > 1) {
+    issue(c1, 0, gsm + ph8::BUF);
+    issue(c1, 2, gsm + ph8::BUF);
+    issue(c1, 3, gsm + ph8::BUF);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();
+
+  bool relax = false;  // a full tile's epilogue stores sit above this step's first waits
+  for (int g = 0; g < G; ++g) {
+    char* cur = gsm + (g & 1) * ph8::BUF;
+    char* nxt = gsm + ((g + 1) & 1) * ph8::BUF;
+    const char* ca = cur;
+    const char* cb = cur + 32768;
+    const bool h1 = g + 1 < G, h2 = g + 2 < G;
+    // ---- phase 0: Q(0,0) — A-lo, B-n0
+    if (h1) issue(c1, 1, nxt);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + mi * 16, kb * 4 + kq);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b0[ni][kb] = ph8::frag(cb, brow + ni * 16, kb * 4 + kq);
+    }
+    if (h1) ph8::vm_wait<10>(relax);  // retire B-n1(g)
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(0, 0, b0)
+    raw_barrier();
+    // ---- phase 1: Q(0,1) — B-n1
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b1[ni][kb] = ph8::frag(cb, brow + 32 + ni * 16, kb * 4 + kq);
+    if (h1) ph8::vm_wait<8>(relax);  // retire A-hi(g)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(0, 1, b1)
+    raw_barrier();
+    // ---- phase 2: Q(1,0) — A-hi; restage A-lo, B-n0 of step g+2
+    if (h2) {
+      issue(c2, 0, cur);
+      issue(c2, 2, cur);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + 64 + mi * 16, kb * 4 + kq);
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PH8_MFMA_QUAD(1, 0, b0)
+    raw_barrier();
+    // ---- phase 3: Q(1,1); restage B-n1 of step g+2; retire A-lo, B-n0 of step g+1
+    if (h2) issue(c2, 3, cur);
+    if (h2) ph8::vm_wait<10>(relax);
+    else if (h1) ph8::vm_wait<4>(relax);
+    raw_barrier();
+    PH8_MFMA_QUAD(1, 1, b1)
+    raw_barrier();
+    relax = false;
+    if (++cc.kt == nk) {  // last K-step of tile cc.i: epilogue while steps g+1, g+2 load
+      ph8::epilogue_reg<EPI>(p, acc, (int)((first + cc.i * stride) / per_batch), cc.row0 + wr * 128,
+                             cc.col0 + wc * 64, lane);
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4)0.0f;
+      relax = relax_ok && cc.row0 + 256 <= p.M && cc.col0 + 256 <= p.N;
+      cc = c1;  // (c1 is tile cc.i + 1 at K-tile 0 here)
+    }
+    c1 = c2;
+    c2 = advance(c2);
+  }
+  if (wr == 0) raw_barrier();  // balance the stagger
+}
+
+template <int EPI>
+int launch_gemm8p(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + 255) / 256;
+  constexpr int LDS = 2 * ph8::BUF;
+  static int n_cu = 0;
+  if (!n_cu) {
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+  }
+  const long long ntiles = (long long)g.tiles_m * g.tiles_n * a->batch;
+  long long grid = ((n_cu + 7) / 8) * 8;
+  while (grid > 8 && grid / 2 >= ntiles) grid /= 2;
+  hipLaunchKernelGGL((gemm8p_kernel<EPI>), dim3((unsigned)grid), dim3(512), LDS, s, g, a->batch);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
 __global__ void splitk_reduce_kernel(const float* part, float* out, long long n, int splits, float beta) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1253,6 +1434,12 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
       if (g_use_glds == 6) return launch_gemm8<1, 0>(k, a, s);
       if (g_use_glds == 7) return launch_gemm8<2, 0>(k, a, s);
       if (g_use_glds == 8) return launch_gemm8<0, -1>(k, a, s);
+      if (g_use_glds == 10) {  // persistent variant (experimental: the epilogue's ordinary loads make hipcc
+                               // drain the prefetch with vmcnt(0) at every K-step; slower until fixed)
+        if (a->act == OCTSAM_ACT_RELU) return launch_gemm8p<OCTSAM_ACT_RELU>(k, a, s);
+        if (a->act == OCTSAM_ACT_GELU) return launch_gemm8p<OCTSAM_ACT_GELU>(k, a, s);
+        return launch_gemm8p<0>(k, a, s);
+      }
       if (a->act == OCTSAM_ACT_RELU) return launch_gemm8<0, OCTSAM_ACT_RELU>(k, a, s);
       if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<0, OCTSAM_ACT_GELU>(k, a, s);
       return launch_gemm8<0, 0>(k, a, s);

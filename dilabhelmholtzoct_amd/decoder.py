@@ -301,6 +301,20 @@ class MaskDecoder(nn.Module):
         K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
         return out
 
+    @staticmethod
+    def _dx(dy_b, w, M, out, *, ldy=None, beta=0.0, ldc=None):
+        """out (+)= dy @ w for w [O, I] bf16. Image-sized M: the NT fast path on a transposed copy of the
+        (small) weight, the accumulation as an in-place residual; token-sized M: the k-major B path."""
+        O, I = w.shape
+        ldy = O if ldy is None else ldy
+        if M >= 65536 and beta in (0.0, 1.0):
+            ldc_ = I if ldc is None else ldc
+            K.gemm(dy_b, w.t().contiguous(), M=M, N=I, K=O, out=out, lda=ldy, ldc=ldc_,
+                   residual=out if beta == 1.0 else None, ldr=ldc_)
+        else:
+            K.gemm(dy_b, w, M=M, N=I, K=O, out=out, b_mode=1, lda=ldy, ldb=I, beta=beta, ldc=ldc)
+        return out
+
     def _lin_bwd(self, dy_b, x_b, wname, bname, M, *, dx_out=None, dx_beta=0.0, ldy=None, ldx=None, x_add=None,
                  x_add_rows=0, wgroup=None, bgroup=None, db_src=None, ldc=None):
         """Backward of y = x W^T + b: dx (optional, accumulate with dx_beta), dW, db."""
@@ -313,7 +327,7 @@ class MaskDecoder(nn.Module):
         O, I = w.shape
         ldy = O if ldy is None else ldy
         if dx_out is not None:
-            K.gemm(dy_b, w, M=M, N=I, K=O, out=dx_out, b_mode=1, lda=ldy, ldb=I, beta=dx_beta, ldc=ldc)
+            self._dx(dy_b, w, M, dx_out, ldy=ldy, beta=dx_beta, ldc=ldc)
         self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
         gb = self.G(bname) if bgroup is None else self._group(self.flat_grad, bgroup, 0)
         src = dy_b if db_src is None else db_src
@@ -495,7 +509,7 @@ class MaskDecoder(nn.Module):
         b2 = self.Bf("upscale_conv2.bias").repeat(4)
         s.up_b1, s.up_b2 = b1, b2
         up1pre = torch.empty(RL, 4 * 64, device=dev, dtype=b16)
-        K.gemm(keys_b, self.W("upscale_conv1.weight"), M=RL, N=256, K=C, out=up1pre, b_mode=1, bias=b1)
+        K.gemm(keys_b, self.W("upscale_conv1.weight").t().contiguous(), M=RL, N=256, K=C, out=up1pre, bias=b1)
         up1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
         mean = torch.empty(RL * 4, device=dev, dtype=f32)
         rstd = torch.empty(RL * 4, device=dev, dtype=f32)
@@ -504,7 +518,8 @@ class MaskDecoder(nn.Module):
         s.up1pre, s.up1, s.up_mean, s.up_rstd = up1pre, up1, mean, rstd
         up2 = torch.empty(RL * 4, 128, device=dev, dtype=b16)
         up2pre = torch.empty(RL * 4, 128, device=dev, dtype=b16)
-        K.gemm(up1, self.W("upscale_conv2.weight"), M=RL * 4, N=128, K=64, out=up2, b_mode=1, bias=b2, act=ACT_GELU,
+        K.gemm(up1, self.W("upscale_conv2.weight").t().contiguous(), M=RL * 4, N=128, K=64, out=up2, bias=b2,
+               act=ACT_GELU,
                pre_out=up2pre)
         s.up2, s.up2pre = up2, up2pre
         masks = torch.empty(P, nsel, 256, 256, device=dev, dtype=f32)
@@ -574,7 +589,7 @@ class MaskDecoder(nn.Module):
         self._qin_bwd(dQ, s.f_qin_b, f + "q_proj.weight", f + "q_proj.bias", R, dq, dtok)
         # d keys2 += [dK | dV] @ [Wk; Wv]
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
-        K.gemm(dKV, wkv, M=RL, N=C, K=2 * CI, out=dkeys, b_mode=1, beta=1.0)
+        self._dx(dKV, wkv, RL, dkeys, beta=1.0)
         self._dw(dKV, s.keys2_b, RL, self.G(f + "k_proj.weight"), ldy=2 * CI, x_add=s.pe_b, x_add_rows=L)
         self._dw(dKV[:, CI:], s.keys2_b, RL, self.G(f + "v_proj.weight"), ldy=2 * CI)
         K.colsum(dKV, RL, 2 * CI, self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
@@ -652,7 +667,7 @@ class MaskDecoder(nn.Module):
                 K.colsum(dV_img, Mi, CI, self.G(t2i + "v_proj.bias"))
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
-                K.gemm(dKQV, wg, M=RL, N=C, K=3 * CI, out=dkeys_in, b_mode=1, beta=1.0)
+                self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)
                 self._dw(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq, C), ldy=3 * CI, x_add=s.pe_b,
                          x_add_rows=L)
                 self._dw(dKQV[:, 2 * CI:], ls.kv_src_b, RL, self.G(t2i + "v_proj.weight"), ldy=3 * CI)

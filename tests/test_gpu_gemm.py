@@ -141,9 +141,9 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     rm[::7] = -1
     rm = rm.to(cuda)
     outs = []
-    # 1: 8-phase kernel (register epilogue; beta != 0 goes to the ring kernel), 8: 8-phase with the LDS-staged
-    # epilogue, 5: persistent ring kernel, 0: generic
-    for fast in (1, 8, 5, 0):
+    # 1: 8-phase kernel, one tile per workgroup (register epilogue; beta != 0 goes to the ring kernel), 10: persistent
+    # 8-phase, 8: 8-phase with the LDS-staged epilogue, 5: persistent ring kernel, 0: generic
+    for fast in (1, 10, 8, 5, 0):
         lib.octsam_gemm_set_fast_path(fast)
         out = C0.clone()
         pout = None if pre is None else torch.zeros(Bt, M, N, device=cuda,
@@ -154,7 +154,7 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
             kw.update(residual=R, stride_r=M * N)
         kernels.gemm(A, W, **kw)
         p8 = 2 if beta == 0.0 else 1
-        assert lib.octsam_gemm_last_path() == {1: p8, 8: p8, 5: 1, 0: 0}[fast]
+        assert lib.octsam_gemm_last_path() == {1: p8, 10: p8, 8: p8, 5: 1, 0: 0}[fast]
         outs.append((out, pout))
     lib.octsam_gemm_set_fast_path(1)
     keep = (rm >= 0).nonzero().flatten()
@@ -175,7 +175,7 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("M,N,K", [(4096, 2304, 768), (1100, 264, 128)])
+@pytest.mark.parametrize("M,N,K", [(4096, 2304, 768), (1100, 264, 128), (70000, 512, 64), (9000, 768, 3072), (20000, 2304, 192)])
 def test_gemm8_register_epilogue_act(cuda, act, M, N, K):
     """8-phase kernel, register epilogue, each activation against torch fp32 (bf16 out, bf16 residual)."""
     from dilabhelmholtzoct_amd import _lib, kernels
