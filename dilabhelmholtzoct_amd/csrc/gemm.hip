@@ -51,6 +51,7 @@ struct GemmK {
   int c_f32, r_f32, pre_f32;
   int conv_c;  // channels for conv3x3 mode
   int tiles_m, tiles_n;
+  int k_total;  // split-K over k-major operands: rows >= k_total (counted from batch 0) read as zero
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -369,9 +370,11 @@ __device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long lon
 // columns past X are clamped to the last chunk (their results are never stored).
 __device__ __forceinline__ int km_off(int r, int ch) { return r * 256 + ((ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 4); }
 
+__device__ uint4 g_zero16[4];  // 16 zero bytes: LDS-DMA source of k rows past the end of a K tail
+
 template <int TX>
 __device__ __forceinline__ void glds_tile_km(const bf16* __restrict__ src, long long ld, int xdim, int x0, int k0,
-                                             char* lds, int wave, int lane) {
+                                             char* lds, int wave, int lane, int kmax = 0x7fffffff) {
   constexpr int NINST = TX / 8;  // 64 rows * TX * 2 B / 1 KiB
 #pragma unroll
   for (int j = wave; j < NINST; j += 8) {
@@ -379,7 +382,7 @@ __device__ __forceinline__ void glds_tile_km(const bf16* __restrict__ src, long 
     const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
     int col = x0 + h * 128 + ch * 8;
     col = col < xdim ? col : xdim - 8;
-    const bf16* g = src + (long long)(k0 + r) * ld + col;
+    const bf16* g = k0 + r < kmax ? src + (long long)(k0 + r) * ld + col : (const bf16*)g_zero16;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(lds + h * 16384 + (j & 15) * 1024), 16, 0, 0);
   }
 }
@@ -545,7 +548,7 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   const int tbeg = xcd * tper, tend = min(ntiles, tbeg + tper);
   const int first = tbeg + loc;
   const int mycnt = first < tend ? (tend - first + nxcd_wg - 1) / nxcd_wg : 0;
-  const int nk = p.K / BK;
+  const int nk = (p.K + BK - 1) / BK;  // (K % BK != 0 only with a k_total tail: zero-filled rows)
   const int total = mycnt * nk;
   if (total == 0) return;
 
@@ -562,9 +565,10 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
     int bz, r0, c0;
     tile_of(i, bz, r0, c0);
     char* st = gsm + (g % NS) * STAGE;
-    if constexpr (AKM) glds_tile_km<BM_>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, wave, lane);
+    const int kmax = p.k_total > 0 ? p.k_total - bz * p.K : 0x7fffffff;
+    if constexpr (AKM) glds_tile_km<BM_>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, wave, lane, kmax);
     else glds_tile<BK>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
-    if constexpr (BKM) glds_tile_km<BN_>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, wave, lane);
+    if constexpr (BKM) glds_tile_km<BN_>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, wave, lane, kmax);
     else glds_tile<BK>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
   };
 
@@ -1362,6 +1366,34 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float4* __res
   }
 }
 
+// 16 float4 columns x 16 split lanes per block, fixed-order combine (deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __restrict__ part, float4* __restrict__ out,
+                                                              long long n4, int splits, float beta) {
+  __shared__ float4 red[16][16];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+#pragma unroll 4
+    for (int j = sl; j < splits; j += 16) {
+      const float4 v = part[(long long)j * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && i < n4) {
+    float4 r = red[0][c];
+#pragma unroll
+    for (int l = 1; l < 16; ++l) { r.x += red[l][c].x; r.y += red[l][c].y; r.z += red[l][c].z; r.w += red[l][c].w; }
+    if (beta != 0.0f) {
+      const float4 o = out[i];
+      r.x += beta * o.x; r.y += beta * o.y; r.z += beta * o.z; r.w += beta * o.w;
+    }
+    out[i] = r;
+  }
+}
+
 }  // namespace
 
 static int g_use_glds = 1;
@@ -1401,6 +1433,10 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   k.sA = a->stride_a; k.sB = a->stride_b; k.sC = a->stride_c; k.sR = a->stride_r;
   k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
   k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
+  k.k_total = a->k_total;
+  OCTSAM_CHECK_ARG(a->k_total == 0 || (a->a_mode == 1 && a->b_mode == 1 && a->k_total <= (long long)a->K * a->batch &&
+                                       a->k_total > (long long)a->K * (a->batch - 1)),
+                   "octsam_gemm: k_total needs a_mode = b_mode = 1 and (batch-1)*K < k_total <= batch*K");
   k.tiles_m = (a->M + BM - 1) / BM;
   k.tiles_n = (a->N + BN - 1) / BN;
   hipStream_t s = (hipStream_t)stream;
@@ -1412,8 +1448,9 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   const bool ok_a = (a->lda & 7) == 0 && (am == 0 || (am == 1 && (a->M & 7) == 0 && a->M >= 8));
   const bool ok_b = (a->ldb & 7) == 0 && (bm == 0 || (bm == 1 && (a->N & 7) == 0 && a->N >= 8));
   const long long tiles = (long long)((a->M + 255) / 256) * ((a->N + 127) / 128) * a->batch;
-  if (g_use_glds && ok_a && ok_b && a->K % 64 == 0 && a->a_blk == 0 && a->b_blk == 0 && fast_epi &&
-      (a->M >= 1024 || tiles >= 64) && ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 &&
+  const bool k_ok = a->K % 64 == 0 || (a->k_total > 0 && a->K % 8 == 0);  // km operands: zero-filled tail
+  if (g_use_glds && ok_a && ok_b && k_ok && a->a_blk == 0 && a->b_blk == 0 && fast_epi &&
+      (a->M >= 1024 || tiles >= 64 || a->k_total > 0) && ((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 &&
       (a->batch == 1 || ((a->stride_a & 7) == 0 && (a->stride_b & 7) == 0))) {
     t_last_path = 1;
     // transposed-read operands need more address registers: the 256x128 tile (no spills)
@@ -1447,6 +1484,7 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
     return launch_glds<256, 64, 2>(k, a, s);
   }
   t_last_path = 0;
+  OCTSAM_CHECK_ARG(a->k_total == 0, "octsam_gemm: k_total tail needs the LDS-DMA path (ld/M/N %% 8, enough tiles)");
   if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);
   if (am == 0 && bm == 1) return launch<0, 1>(k, a->batch, s);
   if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);
@@ -1462,6 +1500,14 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
 extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
                                     void* stream) {
   OCTSAM_CHECK_ARG(partials && out && n > 0 && splits > 0, "octsam_splitk_reduce: bad args");
+  if (n % 4 == 0 && ((uintptr_t)partials & 15) == 0 && ((uintptr_t)out & 15) == 0 && splits >= 32 && n / 4 <= 16384) {
+    // few columns, many splits: 16 float4 columns x 16 split lanes per block
+    long long n4 = n / 4;
+    hipLaunchKernelGGL(splitk_reduce16_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)partials, (float4*)out, n4, splits, beta);
+    OCTSAM_LAUNCH_CHECK("octsam_splitk_reduce");
+    return 0;
+  }
   if (n % 4 == 0 && ((uintptr_t)partials & 15) == 0 && ((uintptr_t)out & 15) == 0 && splits >= 4) {
     long long n4 = n / 4;
     hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, (hipStream_t)stream,

@@ -256,10 +256,14 @@ class MaskDecoder(nn.Module):
 
     @staticmethod
     def _pick_split(Mtok, O, I):
-        """Split-K factor for a weight gradient with Mtok reduction rows: enough (O x I tiles) x splits to fill
-        the chip, chunks a multiple of 64 rows when possible (the persistent kernel's K step), >= 32 rows."""
+        """Split-K (splits, rows per split) for a weight gradient with Mtok reduction rows: enough (O x I tiles)
+        x splits to fill the chip. Mtok % 64 == 0: splits divide Mtok into multiples of 64 rows. Ragged Mtok
+        (token-side rows, e.g. P*7): 64-row multiples, the last split's tail zero-filled (k_total)."""
         tiles = -(-O // 256) * -(-I // 128)
-        aligned = Mtok % 64 == 0
+        if Mtok % 64:
+            want = max(1, min(-(-Mtok // 64), -(-128 // tiles)))
+            ks = 64 * -(-Mtok // (64 * want))
+            return -(-Mtok // ks), ks
         best = 1
         for s in range(1, 513):
             if Mtok % s:
@@ -267,12 +271,12 @@ class MaskDecoder(nn.Module):
             ch = Mtok // s
             if ch < 32:
                 break
-            if aligned and ch % 64:
+            if ch % 64:
                 continue
             best = s
             if tiles * s >= 256:
                 break
-        return best
+        return best, Mtok // best
 
     def _dw(self, dy, x, M, out, *, ldy=None, ldx=None, x_add=None, x_add_rows=0, split=None, accumulate=False):
         """out[o, i] (+)= sum_m dy[m, o] * (x[m, i] (+ x_add[m % rows, i])) -> fp32 (deterministic split-K).
@@ -289,15 +293,16 @@ class MaskDecoder(nn.Module):
             self._dw(S, x_add, rows, out, ldy=O, ldx=ldx, accumulate=True)
             return out
         if split is None:
-            split = self._pick_split(M, O, I)
+            split, Ks = self._pick_split(M, O, I)
+        else:
+            Ks = M // split
         beta = 1.0 if accumulate else 0.0
-        if split == 1:
+        if split == 1 and Ks == M:
             K.gemm(dy, x, M=O, N=I, K=M, out=out, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, beta=beta)
             return out
-        Ks = M // split
         part = torch.empty((split, O, I), device=out.device, dtype=torch.float32)
         K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, batch=split,
-               stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I)
+               stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I, k_total=M if Ks * split != M else 0)
         K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
         return out
 

@@ -24,7 +24,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
          stride_a: int = 0, stride_b: int = 0, stride_c: int = 0, stride_r: int = 0,
          A2: torch.Tensor | None = None, B2: torch.Tensor | None = None, a2_rows: int = 0,
          b2_rows: int = 0, conv_c: int = 0, a_remap: tuple[int, int] = (0, 1),
-         b_remap: tuple[int, int] = (0, 1), r_remap: tuple[int, int] = (0, 1)) -> torch.Tensor:
+         b_remap: tuple[int, int] = (0, 1), r_remap: tuple[int, int] = (0, 1), k_total: int = 0) -> torch.Tensor:
     """C[b] = epi(alpha * A[b] @ B[b]^T); see octsam_gemm in include/octsam.h."""
     _require_cuda(A, B, out, bias, residual, pre_out, row_map, A2, B2)
     if a_mode in (0, 4):
@@ -49,7 +49,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         r_f32=int(residual is not None and residual.dtype == torch.float32),
         pre_f32=int(pre_out is not None and pre_out.dtype == torch.float32),
         conv_c=conv_c, a2_rows=a2_rows, b2_rows=b2_rows, a_blk=a_remap[0], a_rep=a_remap[1],
-        b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1])
+        b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total)
     _lib.call("octsam_gemm", ctypes.byref(args))
     return out
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 1
+#define OCTSAM_ABI_VERSION 2
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -72,6 +72,9 @@ typedef struct octsam_gemm_args {
   int32_t conv_c;
   int32_t a2_rows, b2_rows;
   int32_t a_blk, a_rep, b_blk, b_rep, r_blk, r_rep;
+  /* k-major A and B (a_mode = b_mode = 1) batched as split-K over one [k_total][*] operand pair:
+     batch b covers rows [b*K, (b+1)*K) and rows >= k_total read as zero (0 = no tail). */
+  int32_t k_total;
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);

@@ -218,3 +218,19 @@ def test_gemm_fast_path_kmajor(cuda, a_mode, b_mode, shape):
         assert (lib.octsam_gemm_last_path() > 0) == bool(fast)
         assert _rel(out, ref) < 1e-5, (fast, _rel(out, ref))
     lib.octsam_gemm_set_fast_path(1)
+
+
+@pytest.mark.parametrize("Mtok,O,I", [(1176, 256, 256), (168, 32, 256), (1176, 2048, 256), (1176, 128, 256)])
+def test_dw_ragged_splitk(cuda, Mtok, O, I):
+    """Weight gradient over a ragged token count (P*7 rows): 64-row split-K chunks, the last chunk's tail
+    zero-filled by the k-major loaders (k_total), fixed-order combine."""
+    from dilabhelmholtzoct_amd.decoder import MaskDecoder
+    g = torch.Generator().manual_seed(Mtok + O)
+    dy = torch.randn(Mtok, O, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(Mtok, I, generator=g).to(cuda, torch.bfloat16)
+    out = torch.empty(O, I, device=cuda)
+    split, ks = MaskDecoder._pick_split(Mtok, O, I)
+    assert split * ks >= Mtok and (split - 1) * ks < Mtok and ks % 64 == 0
+    MaskDecoder._dw(MaskDecoder, dy, x, Mtok, out)
+    ref = dy.float().t() @ x.float()
+    assert _rel(out, ref) < 1e-5
