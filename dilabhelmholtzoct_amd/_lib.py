@@ -70,11 +70,12 @@ _SIGNATURES = {
                                           c_void_p]),
     "octsam_dec_tok_attn_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                                           c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_dec_t2i_workspace": (c_int64, [c_int32, c_int32]),
     "octsam_dec_t2i_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
-                                     c_void_p, c_void_p, c_void_p]),
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_dec_t2i_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                     c_void_p]),
+                                     c_void_p, c_void_p]),
     "octsam_dec_i2t_fwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                      c_void_p, c_int64, c_void_p]),
     "octsam_dec_i2t_bwd_partials": (c_int64, [c_int32, c_int32, c_int32]),

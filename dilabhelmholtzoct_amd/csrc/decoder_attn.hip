@@ -100,324 +100,469 @@ __global__ __launch_bounds__(256) void tok_attn_bwd_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------------------- t2i
-// XCD-aware (prompt, head) decode: the 8 heads of a prompt share one XCD (same K/V rows in L2).
-__device__ __forceinline__ void t2i_decode(int id, int& p, int& h) {
-  p = (id & 7) + 8 * (id >> 6);
-  h = (id >> 3) & 7;
+// Token -> image attention: per prompt Tq <= 8 queries x 8 heads x 16 dims against L = 4096 keys,
+// flash-decoding on MFMA. A workgroup = (prompt, 512-key chunk); wave w owns the head pair (2w, 2w+1).
+// The pair's 64-B slices of the K and V rows stream into a wave-private LDS ring by LDS-DMA
+// (global_load_lds, 32 keys per step, 3 steps in flight). One v_mfma_f32_16x16x32_bf16 per 16 keys
+// gives the scores of BOTH heads: A = the K rows (32 dims = 2 heads), B = the queries block-diagonally
+// (column n < 8: query n of head 2w with the other head's dims zero; n >= 8: query n-8 of head 2w+1),
+// so the transposed score tile S^T[key][n] has one (query, head) per lane column and the online softmax
+// is per lane (+ two xor-shuffles for the tile max). P^T (bf16) is the B operand of O^T += V^T P^T,
+// V^T read with ds_read_b64_tr_b16. The queries are split hi + lo bf16 (two MFMAs), so scores keep
+// ~16 mantissa bits. Per-chunk (m, l, O) partials are merged in fixed order by t2i_combine_kernel.
+// Backward recomputes P from the forward's log-sum-exp in both orientations (S^T for dQ, S for dK/dV,
+// each two MFMAs) so that every product takes its operands without a register transpose.
+namespace t2 {
+constexpr int CHUNK = 512, STEP = 32, RING = 4;
+constexpr int STEP_BYTES = 2 * STEP * 64;    // K + V: 32 rows x 64 B each
+constexpr int WAVE_LDS = RING * STEP_BYTES;  // 16 KiB per wave
+constexpr int SMEM = 4 * WAVE_LDS;
+constexpr int PART = 16 * 16 + 16 + 16;      // fwd: O[n][d], m[n], l[n] per (prompt, chunk, pair); bwd: dQ[n][d]
+constexpr float L2E = 1.4426950408889634f;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 16-B chunk swizzles: K image (row reads) chunk ^ ((r>>2)&3); V image (transposed reads) chunk ^ 2((r>>2)&1)
+__device__ __forceinline__ int ksw(int r, int c) { return c ^ ((r >> 2) & 3); }
+__device__ __forceinline__ int vsw(int r, int c) { return c ^ (((r >> 2) & 1) << 1); }
+
+// rows key0 .. key0+31 of the pair's K and V slices -> ring slot: 4 LDS-DMA instructions of 1 KiB
+__device__ __forceinline__ void load_step(const bf16* kb, long long ldk, const bf16* vb, long long ldv, int key0,
+                                          char* slot, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * i + (lane >> 2), pc = lane & 3;
+    __builtin_amdgcn_global_load_lds((const void*)(kb + (long long)(key0 + r) * ldk + 8 * ksw(r, pc)),
+                                     (lds_ptr_t)(slot + 1024 * i), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vb + (long long)(key0 + r) * ldv + 8 * vsw(r, pc)),
+                                     (lds_ptr_t)(slot + 2048 + 1024 * i), 16, 0, 0);
+  }
 }
 
-// q fp32 [P,Tq,128]; k,v bf16 rows (kv block b = p / kv_rep) [*, L, ldkv]; out bf16 [P,Tq,128]; lse [P,8,Tq]
-__global__ __launch_bounds__(MAXT * 64) void t2i_fwd_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
-                                                            const bf16* __restrict__ v, long long ldkv, int kv_rep,
-                                                            int P, int Tq, int L, bf16* __restrict__ out,
-                                                            float* __restrict__ lse) {
-  int p, h;
-  t2i_decode(blockIdx.x, p, h);
-  if (p >= P) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave >= Tq) return;
+// rows of a 16-key tile as an MFMA row operand: lane (g, c) = row 16t + c, pair dims 8g .. 8g+7
+__device__ __forceinline__ bf16x8 row_op(const char* img, int t, bool vimg, int lane) {
+  const int r = 16 * t + (lane & 15), g = lane >> 4;
+  return *(const bf16x8*)(img + 64 * r + 16 * (vimg ? vsw(r, g) : ksw(r, g)));
+}
+// transposed: element q of lane (g, c) = X[16t + 4g + q][dim 16 hl + c]
+__device__ __forceinline__ s16x4 tr_op(const char* img, int t, int hl, bool vimg, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r = 16 * t + 4 * g + q, lc = 2 * hl + (p >> 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(img + 64 * r + 16 * (vimg ? vsw(r, lc) : ksw(r, lc)) + 8 * (p & 1)));
+}
+
+// Block-diagonal token operand (x fp32 [P, Tq, 128]): lane (g, c), element j = pair dim 8g + j of column
+// n = c (n < 8: token n of head 2hp; n >= 8: token n-8 of head 2hp+1); zero off the diagonal / n >= Tq.
+__device__ __forceinline__ void tok_op(const float* x, int p, int Tq, int hp, float scale, int lane, bf16x8& hi,
+                                       bf16x8& lo) {
+  const int g = lane >> 4, c = lane & 15, qi = c & 7;
+  const bool on = (g >> 1) == (c >> 3) && qi < Tq;
+  const float* src = x + ((long long)p * Tq + (on ? qi : 0)) * 128 + hp * 32 + 8 * g;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = on ? src[j] * scale : 0.0f;
+    hi[j] = (bf16)v;
+    lo[j] = (bf16)(v - (float)hi[j]);
+  }
+}
+
+// 16x16x16 operand "X_h^T": lane (g, c), element j = x[token n = 4g+j (head 2hp+hl: n in [8hl, 8hl+8))][16h + c]
+__device__ __forceinline__ s16x4 tokT_op(const float* x, int p, int Tq, int hp, int hl, float scale, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  s16x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = 4 * g + j, qi = n & 7;
+    const bool on = (n >> 3) == hl && qi < Tq;
+    const float v = on ? x[((long long)p * Tq + qi) * 128 + (2 * hp + hl) * 16 + c] * scale : 0.0f;
+    r[j] = __builtin_bit_cast(short, (bf16)v);
+  }
+  return r;
+}
+
+__device__ __forceinline__ s16x4 pack4(const f32x4& a) {
+  s16x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = __builtin_bit_cast(short, (bf16)a[i]);
+  return r;
+}
+__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(s16x4 a, s16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in {0, 4, ..., 60}
+__device__ __forceinline__ void wait_vm(int n) {
+#define T2_W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    T2_W(0) T2_W(4) T2_W(8) T2_W(12) T2_W(16) T2_W(20) T2_W(24) T2_W(28) T2_W(32) T2_W(36) T2_W(40) T2_W(44)
+    T2_W(48) T2_W(52) T2_W(56) default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+  }
+#undef T2_W
+}
+}  // namespace t2
+
+// q fp32 [P,Tq,128]; k, v bf16 rows [(p / kv_rep) * L + key] * ldkv; part fp32 [P][nchunk][4][PART]
+__global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
+                                                      const bf16* __restrict__ v, long long ldkv, int kv_rep, int Tq,
+                                                      int L, int nchunk, float* __restrict__ part) {
+  using namespace t2;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6;
+  const int p = blockIdx.x / nchunk, chunk = blockIdx.x - p * nchunk;
+  const int key0 = chunk * CHUNK;
+  const int nstep = min(CHUNK, L - key0) / STEP;
+  char* ring = tsm + hp * WAVE_LDS;
   const long long kvb = (long long)(p / kv_rep) * L;
-  float qr[16];
+  const bf16* kb = k + kvb * ldkv + hp * 32;
+  const bf16* vb = v + kvb * ldkv + hp * 32;
+  bf16x8 qhi, qlo;
+  tok_op(q, p, Tq, hp, 0.25f * L2E, lane, qhi, qlo);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loop's counted waits see only the ring's loads
+  for (int s = 0; s < RING - 1 && s < nstep; ++s) load_step(kb, ldkv, vb, ldkv, key0 + s * STEP, ring + s * STEP_BYTES, lane);
+  f32x4 o0 = (f32x4)0.0f, o1 = (f32x4)0.0f;
+  float m = -INFINITY, l = 0.0f;
+  for (int s = 0; s < nstep; ++s) {
+    if (s + RING - 1 < nstep) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's previous reads are done
+      load_step(kb, ldkv, vb, ldkv, key0 + (s + RING - 1) * STEP, ring + ((s + RING - 1) % RING) * STEP_BYTES, lane);
+    }
+    wait_vm(4 * min(RING - 1, nstep - 1 - s));
+    const char* slot = ring + (s % RING) * STEP_BYTES;
+    f32x4 st[2];
 #pragma unroll
-  for (int d = 0; d < 16; ++d) qr[d] = q[((long long)p * Tq + wave) * 128 + h * 16 + d] * 0.25f;
-  float m = -INFINITY, l = 0.0f, o[16];
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 kf = row_op(slot, t, false, lane);
+      st[t] = mfma32(kf, qhi, (f32x4)0.0f);
+      st[t] = mfma32(kf, qlo, st[t]);
+    }
+    float mx = fmaxf(fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3])),
+                     fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    f32x4 e0, e1;
 #pragma unroll
-  for (int d = 0; d < 16; ++d) o[d] = 0.0f;
-  for (int key = lane; key < L; key += 64) {
-    const bf16* kr = k + (kvb + key) * ldkv + h * 16;
-    const bf16* vr = v + (kvb + key) * ldkv + h * 16;
-    bf16x8 k0 = *(const bf16x8*)kr, k1 = *(const bf16x8*)(kr + 8);
+    for (int i = 0; i < 4; ++i) {
+      e0[i] = __builtin_amdgcn_exp2f(st[0][i] - mn);
+      e1[i] = __builtin_amdgcn_exp2f(st[1][i] - mn);
+    }
+    l = fmaf(l, alpha, (e0[0] + e0[1]) + (e0[2] + e0[3]) + (e1[0] + e1[1]) + (e1[2] + e1[3]));
+    o0 *= alpha;
+    o1 *= alpha;
+    const bf16x8 pf = cat8(pack4(e0), pack4(e1));
+    const char* vimg = slot + 2048;
+    o0 = mfma32(cat8(tr_op(vimg, 0, 0, true, lane), tr_op(vimg, 1, 0, true, lane)), pf, o0);
+    o1 = mfma32(cat8(tr_op(vimg, 0, 1, true, lane), tr_op(vimg, 1, 1, true, lane)), pf, o1);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * PART;
+  const int c = lane & 15;
+  *(f32x4*)(w + c * 16 + 4 * (lane >> 4)) = c < 8 ? o0 : o1;  // O^T[d = 4g+i][n = c] -> O[n][d]
+  if (lane < 16) {
+    w[256 + lane] = m;
+    w[272 + lane] = l;
+  }
+}
+
+// merge the chunk partials in chunk order: out bf16 [P,Tq,128], lse fp32 [P,8,Tq] (natural log)
+__global__ void t2i_combine_kernel(const float* __restrict__ part, int nchunk, int Tq, bf16* __restrict__ out,
+                                   float* __restrict__ lse) {
+  using namespace t2;
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int d = t & 15, hq = t >> 4, h = hq / Tq, qi = hq - h * Tq;
+  const int n = (h & 1) * 8 + qi;
+  const float* w = part + ((long long)p * nchunk * 4 + (h >> 1)) * PART;
+  float M = -INFINITY;
+  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, w[(long long)c * 4 * PART + 256 + n]);
+  float Ls = 0.0f, O = 0.0f;
+  for (int c = 0; c < nchunk; ++c) {
+    const float* wc = w + (long long)c * 4 * PART;
+    const float e = __builtin_amdgcn_exp2f(wc[256 + n] - M);
+    Ls = fmaf(e, wc[272 + n], Ls);
+    O = fmaf(e, wc[n * 16 + d], O);
+  }
+  out[((long long)p * Tq + qi) * 128 + h * 16 + d] = (bf16)(O / Ls);
+  if (d == 0) lse[((long long)p * 8 + h) * Tq + qi] = (M + __log2f(Ls)) / L2E;
+}
+
+// Backward. dout fp32 [P,Tq,128], out bf16 (forward output), lse [P,8,Tq]; writes per-prompt dk, dv bf16
+// [P*L, lddkv] (head slice 16h) and dQ partials part[P][nchunk][4][256] (reduced by t2i_dq_kernel).
+__global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
+                                                      const bf16* __restrict__ v, long long ldkv, int kv_rep, int Tq,
+                                                      int L, int nchunk, const bf16* __restrict__ out,
+                                                      const float* __restrict__ dout, const float* __restrict__ lse,
+                                                      bf16* __restrict__ dk, bf16* __restrict__ dv, long long lddkv,
+                                                      float* __restrict__ part) {
+  using namespace t2;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int p = blockIdx.x / nchunk, chunk = blockIdx.x - p * nchunk;
+  const int key0 = chunk * CHUNK;
+  const int nstep = min(CHUNK, L - key0) / STEP;
+  char* ring = tsm + hp * WAVE_LDS;
+  const long long kvb = (long long)(p / kv_rep) * L;
+  const bf16* kb = k + kvb * ldkv + hp * 32;
+  const bf16* vb = v + kvb * ldkv + hp * 32;
+  bf16x8 qhi, qlo, dop, dlo;
+  tok_op(q, p, Tq, hp, 0.25f * L2E, lane, qhi, qlo);
+  tok_op(dout, p, Tq, hp, 1.0f, lane, dop, dlo);
+  s16x4 adO[2], aQ[2];
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) {
+    adO[hl] = tokT_op(dout, p, Tq, hp, hl, 1.0f, lane);
+    aQ[hl] = tokT_op(q, p, Tq, hp, hl, 0.25f, lane);
+  }
+  // row constants of token n (log2-domain lse; delta = dO . O): column n = c (S^T) and rows n = 4g+i (S)
+  auto tok_consts = [&](int n, float& l2, float& del) {
+    const int qi = n & 7, h = 2 * hp + (n >> 3);
+    if (qi >= Tq) {
+      l2 = INFINITY;
+      del = 0.0f;
+      return;
+    }
+    l2 = lse[((long long)p * 8 + h) * Tq + qi] * L2E;
+    const float* a = dout + ((long long)p * Tq + qi) * 128 + h * 16;
+    const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
     float s = 0.0f;
 #pragma unroll
-    for (int d = 0; d < 8; ++d) s += qr[d] * (float)k0[d] + qr[8 + d] * (float)k1[d];
-    float mn = fmaxf(m, s);
-    float a = __expf(m - mn), e = __expf(s - mn);
-    bf16x8 v0 = *(const bf16x8*)vr, v1 = *(const bf16x8*)(vr + 8);
+    for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+    del = s;
+  };
+  float lc2, dc;
+  tok_consts(c, lc2, dc);
+  float lr2[4], dr[4];
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      o[d] = o[d] * a + e * (float)v0[d];
-      o[8 + d] = o[8 + d] * a + e * (float)v1[d];
+  for (int i = 0; i < 4; ++i) tok_consts(4 * g + i, lr2[i], dr[i]);
+  f32x4 dq0 = (f32x4)0.0f, dq1 = (f32x4)0.0f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loop's counted waits see only the ring and its stores
+  for (int s = 0; s < RING - 1 && s < nstep; ++s) load_step(kb, ldkv, vb, ldkv, key0 + s * STEP, ring + s * STEP_BYTES, lane);
+  for (int s = 0; s < nstep; ++s) {
+    if (s + RING - 1 < nstep) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      load_step(kb, ldkv, vb, ldkv, key0 + (s + RING - 1) * STEP, ring + ((s + RING - 1) % RING) * STEP_BYTES, lane);
     }
-    l = l * a + e;
-    m = mn;
-  }
-  const float M = wave_max(m);
-  const float f = (m == -INFINITY) ? 0.0f : __expf(m - M);
-  l = wave_sum(l * f);
+    // LDS-DMA loads and global stores share vmcnt; issued after step s's loads: the loads of steps
+    // s+1 .. s+3 and the 8 stores of each of the steps max(0, s-3) .. s-1
+    wait_vm(4 * min(RING - 1, nstep - 1 - s) + 8 * min(RING - 1, s));
+    const char* slot = ring + (s % RING) * STEP_BYTES;
+    const char* vimg = slot + 2048;
 #pragma unroll
-  for (int d = 0; d < 16; ++d) o[d] = wave_sum(o[d] * f);
-  if (lane < 16) {
-    float val = 0.0f;
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 kf = row_op(slot, t, false, lane), vf = row_op(vimg, t, true, lane);
+      f32x4 sT = mfma32(kf, qhi, (f32x4)0.0f);
+      sT = mfma32(kf, qlo, sT);                     // S^T[key 4g+i][n c]
+      const f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);
+      f32x4 sS = mfma32(qhi, kf, (f32x4)0.0f);
+      sS = mfma32(qlo, kf, sS);                     // S[n 4g+i][key c]
+      const f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+      f32x4 dsT, pS, dsS;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) val = (lane == d) ? o[d] : val;
-    out[((long long)p * Tq + wave) * 128 + h * 16 + lane] = (bf16)(val / l);
+      for (int i = 0; i < 4; ++i) {
+        dsT[i] = __builtin_amdgcn_exp2f(sT[i] - lc2) * (dpT[i] - dc);
+        pS[i] = __builtin_amdgcn_exp2f(sS[i] - lr2[i]);
+        dsS[i] = pS[i] * (dpS[i] - dr[i]);
+      }
+      const s16x4 pSb = pack4(pS), dsSb = pack4(dsS), dsTb = pack4(dsT);
+      const long long row = ((long long)p * L + key0 + s * STEP + 16 * t + c) * lddkv + 32 * hp + 4 * g;
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        const f32x4 dvt = mfma16(adO[hl], pSb, (f32x4)0.0f);  // dV^T[d 4g+i][key c]
+        const f32x4 dkt = mfma16(aQ[hl], dsSb, (f32x4)0.0f);  // dK^T[d 4g+i][key c]
+        *(s16x4*)(dv + row + 16 * hl) = pack4(dvt);
+        *(s16x4*)(dk + row + 16 * hl) = pack4(dkt);
+      }
+      dq0 = mfma16(dsTb, tr_op(slot, t, 0, false, lane), dq0);  // dQ[n 4g+i][d c] (head 2hp)
+      dq1 = mfma16(dsTb, tr_op(slot, t, 1, false, lane), dq1);  // (head 2hp+1)
+    }
   }
-  if (lane == 0) lse[((long long)p * 8 + h) * Tq + wave] = M + __logf(l);
+  float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * 256;
+  const f32x4 dqs = g < 2 ? dq0 : dq1;  // rows n < 8 belong to head 2hp, n >= 8 to head 2hp+1
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[(4 * g + i) * 16 + c] = dqs[i];
 }
 
-// Backward: one block per (prompt, head), 256 threads; keys in chunks of 256 (one per thread).
-// dq bf16 [P,Tq,128]; dk, dv bf16 per prompt [P, L, lddkv] (head slice h*16)
-__global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
-                                                      const bf16* __restrict__ v, long long ldkv, int kv_rep, int P,
-                                                      int Tq, int L, const bf16* __restrict__ out,
-                                                      const float* __restrict__ dout, const float* __restrict__ lse,
-                                                      bf16* __restrict__ dq, bf16* __restrict__ dk,
-                                                      bf16* __restrict__ dv, long long lddkv) {
-  int p, h;
-  t2i_decode(blockIdx.x, p, h);
-  if (p >= P) return;
-  __shared__ float sq[MAXT][16], sdo[MAXT][16], sD[MAXT], sL[MAXT];
-  __shared__ float sds[256][MAXT + 1];
-  __shared__ float skf[256][17];
-  __shared__ float red[2][MAXT * 16];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < Tq * 16; e += 256) {
-    int i = e / 16, d = e % 16;
-    sq[i][d] = q[((long long)p * Tq + i) * 128 + h * 16 + d] * 0.25f;
-    sdo[i][d] = dout[((long long)p * Tq + i) * 128 + h * 16 + d];
-  }
-  if (tid < Tq) {
-    float acc = 0.0f;
-    for (int d = 0; d < 16; ++d)
-      acc += dout[((long long)p * Tq + tid) * 128 + h * 16 + d] * (float)out[((long long)p * Tq + tid) * 128 + h * 16 + d];
-    sD[tid] = acc;
-    sL[tid] = lse[((long long)p * 8 + h) * Tq + tid];
-  }
-  __syncthreads();
-  const long long kvb = (long long)(p / kv_rep) * L;
-  // phase-2 owner: (i, d, half) -> sums 128 of the chunk's 256 keys
-  const int oi = (tid >> 1) / 16, od = (tid >> 1) % 16, ohalf = tid & 1;
-  float dq_acc = 0.0f;
-  for (int c0 = 0; c0 < L; c0 += 256) {
-    const int key = c0 + tid;
-    if (key < L) {
-      const bf16* kr = k + (kvb + key) * ldkv + h * 16;
-      const bf16* vr = v + (kvb + key) * ldkv + h * 16;
-      float kf[16], vf[16];
-      bf16x8 k0 = *(const bf16x8*)kr, k1 = *(const bf16x8*)(kr + 8);
-      bf16x8 v0 = *(const bf16x8*)vr, v1 = *(const bf16x8*)(vr + 8);
-#pragma unroll
-      for (int d = 0; d < 8; ++d) { kf[d] = (float)k0[d]; kf[8 + d] = (float)k1[d]; vf[d] = (float)v0[d]; vf[8 + d] = (float)v1[d]; }
-      float dka[16], dva[16];
-#pragma unroll
-      for (int d = 0; d < 16; ++d) { dka[d] = 0.0f; dva[d] = 0.0f; skf[tid][d] = kf[d]; }
-#pragma unroll
-      for (int i = 0; i < MAXT; ++i) {
-        float ds = 0.0f;
-        if (i < Tq) {
-          float s = 0.0f, dp = 0.0f;
-#pragma unroll
-          for (int d = 0; d < 16; ++d) { s += sq[i][d] * kf[d]; dp += sdo[i][d] * vf[d]; }
-          float pr = __expf(s - sL[i]);
-          ds = pr * (dp - sD[i]);
-#pragma unroll
-          for (int d = 0; d < 16; ++d) {
-            dva[d] += pr * sdo[i][d];
-            dka[d] += ds * sq[i][d];
-          }
-        }
-        sds[tid][i] = ds;
-      }
-      bf16x8 o0, o1, w0, w1;
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        o0[d] = (bf16)dka[d]; o1[d] = (bf16)dka[8 + d];
-        w0[d] = (bf16)dva[d]; w1[d] = (bf16)dva[8 + d];
-      }
-      bf16* dkr = dk + ((long long)p * L + key) * lddkv + h * 16;
-      bf16* dvr = dv + ((long long)p * L + key) * lddkv + h * 16;
-      *(bf16x8*)dkr = o0; *(bf16x8*)(dkr + 8) = o1;
-      *(bf16x8*)dvr = w0; *(bf16x8*)(dvr + 8) = w1;
-    } else {
-#pragma unroll
-      for (int i = 0; i < MAXT; ++i) sds[tid][i] = 0.0f;
-#pragma unroll
-      for (int d = 0; d < 16; ++d) skf[tid][d] = 0.0f;
-    }
-    __syncthreads();
-    if (oi < Tq) {
-      float a = 0.0f;
-      for (int t = ohalf * 128; t < ohalf * 128 + 128; ++t) a += sds[t][oi] * skf[t][od];
-      dq_acc += a;
-    }
-    __syncthreads();
-  }
-  if (oi < Tq) red[ohalf][oi * 16 + od] = dq_acc;
-  __syncthreads();
-  for (int e = tid; e < Tq * 16; e += 256) {
-    int i = e / 16, d = e % 16;
-    // ds was formed with the scaled q; d(s)/d(q) = 0.25 * k
-    dq[((long long)p * Tq + i) * 128 + h * 16 + d] = (bf16)((red[0][e] + red[1][e]) * 0.25f);
-  }
+// dq bf16 [P,Tq,128] = 0.25 * sum over chunks (in order) of the dQ partials
+__global__ void t2i_dq_kernel(const float* __restrict__ part, int nchunk, int Tq, bf16* __restrict__ dq) {
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int d = t & 15, hq = t >> 4, h = hq / Tq, qi = hq - h * Tq;
+  const int n = (h & 1) * 8 + qi;
+  const float* w = part + ((long long)p * nchunk * 4 + (h >> 1)) * 256 + n * 16 + d;
+  float s = 0.0f;
+  for (int c = 0; c < nchunk; ++c) s += w[(long long)c * 4 * 256];
+  dq[((long long)p * Tq + qi) * 128 + h * 16 + d] = (bf16)(0.25f * s);
 }
 
 // ---------------------------------------------------------------------------------------- i2t
-constexpr int I2T_ROWS = 256;  // image rows per block
+// Image -> token attention: L = 4096 image-row queries x Tk <= 8 token keys, 8 heads x 16. The t2i
+// scheme with the roles swapped: a workgroup = (prompt, 512-row chunk), one wave per head pair; the token
+// keys/values are constant block-diagonal operands, the image rows the streamed ones. The score tile is
+// taken transposed, S^T[token n][row r] (softmax over a head's 8 token slots: in-lane + one xor-16
+// shuffle), and O^T = V^T P^T. Backward also forms S[r][n] (two more MFMAs) for dK^T = Q^T dS and
+// dV^T = dO^T P, whose Q^T / dO^T operands are ds_read_b64_tr_b16 reads of the rows staged by LDS-DMA;
+// the per-row softmax statistics move from the S^T to the S layout by ds_bpermute. dK / dV partials per
+// (chunk, prompt) are reduced in fixed order by octsam_splitk_reduce.
+namespace i2 {
+constexpr int CHUNK = 512;
+}
 
-// q bf16 rows (q block b = p / q_rep) [*, L, ldq]; k, v fp32 [P, Tk, 128]; out bf16 [P, L, ldo]
+// q bf16 rows [(p / q_rep) * L + r] * ldq; k, v fp32 [P, Tk, 128]; out bf16 [P*L, ldo]
 __global__ __launch_bounds__(256) void i2t_fwd_kernel(const bf16* __restrict__ q, long long ldq, int q_rep,
                                                       const float* __restrict__ k, const float* __restrict__ v, int Tk,
-                                                      int L, bf16* __restrict__ out, long long ldo) {
-  const int p = blockIdx.y;
-  const int r0 = blockIdx.x * I2T_ROWS;
-  __shared__ float sk[MAXT][128], sv[MAXT][128];
-  for (int e = threadIdx.x; e < Tk * 128; e += 256) {
-    sk[e / 128][e % 128] = k[(long long)p * Tk * 128 + e] * 0.25f;
-    sv[e / 128][e % 128] = v[(long long)p * Tk * 128 + e];
-  }
-  __syncthreads();
-  const int h = threadIdx.x & 7;
-  const long long qb = (long long)(p / q_rep) * L;
-  for (int r = r0 + (threadIdx.x >> 3); r < r0 + I2T_ROWS && r < L; r += 32) {
-    const bf16* qr = q + (qb + r) * ldq + h * 16;
-    bf16x8 a0 = *(const bf16x8*)qr, a1 = *(const bf16x8*)(qr + 8);
-    float qf[16];
+                                                      int L, int nchunk, bf16* __restrict__ out, long long ldo) {
+  using namespace t2;
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int p = blockIdx.x / nchunk, chunk = blockIdx.x - p * nchunk;
+  const int r0 = chunk * i2::CHUNK;
+  const int ntile = min(i2::CHUNK, L - r0) / 16;
+  bf16x8 khi, klo;
+  tok_op(k, p, Tk, hp, 0.25f * L2E, lane, khi, klo);  // [n = c][pair dim 8g+j]
+  s16x4 av[2];
 #pragma unroll
-    for (int d = 0; d < 8; ++d) { qf[d] = (float)a0[d]; qf[8 + d] = (float)a1[d]; }
-    float s[MAXT];
+  for (int hl = 0; hl < 2; ++hl) av[hl] = tokT_op(v, p, Tk, hp, hl, 1.0f, lane);  // V_h^T [d = c][n = 4g+j]
+  bool nv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) nv[i] = ((4 * g + i) & 7) < Tk;
+  const bf16* qb = q + ((long long)(p / q_rep) * L + r0) * ldq + hp * 32 + 8 * g;
+  bf16* ob = out + ((long long)p * L + r0) * ldo + hp * 32 + 4 * g;
+  bf16x8 qf = *(const bf16x8*)(qb + (long long)c * ldq);
+  for (int t = 0; t < ntile; ++t) {
+    bf16x8 qn = qf;
+    if (t + 1 < ntile) qn = *(const bf16x8*)(qb + (long long)(16 * (t + 1) + c) * ldq);
+    f32x4 s = mfma32(khi, qf, (f32x4)0.0f);
+    s = mfma32(klo, qf, s);  // S^T[n 4g+i][r c]
     float mx = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < MAXT; ++j) {
-      if (j < Tk) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) acc += qf[d] * sk[j][h * 16 + d];
-        s[j] = acc;
-        mx = fmaxf(mx, acc);
-      }
-    }
+    for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, s[i]) : mx;
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    f32x4 e;
     float sum = 0.0f;
 #pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) { s[j] = __expf(s[j] - mx); sum += s[j]; }
-    const float inv = 1.0f / sum;
-    float o[16];
+    for (int i = 0; i < 4; ++i) {
+      e[i] = nv[i] ? __builtin_amdgcn_exp2f(s[i] - mx) : 0.0f;
+      sum += e[i];
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    e *= 1.0f / sum;
+    const s16x4 pb = pack4(e);
 #pragma unroll
-    for (int d = 0; d < 16; ++d) o[d] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) {
-        float pr = s[j] * inv;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) o[d] += pr * sv[j][h * 16 + d];
-      }
-    bf16x8 o0, o1;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) { o0[d] = (bf16)o[d]; o1[d] = (bf16)o[8 + d]; }
-    bf16* orow = out + ((long long)p * L + r) * ldo + h * 16;
-    *(bf16x8*)orow = o0;
-    *(bf16x8*)(orow + 8) = o1;
+    for (int hl = 0; hl < 2; ++hl)
+      *(s16x4*)(ob + (long long)(16 * t + c) * ldo + 16 * hl) = pack4(mfma16(av[hl], pb, (f32x4)0.0f));
+    qf = qn;
   }
 }
 
-// Backward. dout bf16 [P, L, lddo]; writes dq bf16 [P, L, lddq] and per-block partials
-// part[blk][P][2][Tk][128] (dk then dv), blk = blockIdx.x (L / 256 blocks per prompt).
+// Backward. dout bf16 [P*L, lddo]; writes dq bf16 [P*L, lddq] and partials fp32 [nchunk][P][2][Tk][128]
+// (dk; dv).
 __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q, long long ldq, int q_rep,
                                                       const float* __restrict__ k, const float* __restrict__ v, int Tk,
-                                                      int L, const bf16* __restrict__ dout, long long lddo,
+                                                      int L, int nchunk, const bf16* __restrict__ dout, long long lddo,
                                                       bf16* __restrict__ dq, long long lddq, float* __restrict__ part,
                                                       int P) {
-  const int p = blockIdx.y;
-  const int r0 = blockIdx.x * I2T_ROWS;
-  __shared__ float sk[MAXT][128], sv[MAXT][128];
-  __shared__ float sds[32][8][MAXT], spr[32][8][MAXT];
-  __shared__ float sq[32][128], sdo[32][128];
-  for (int e = threadIdx.x; e < Tk * 128; e += 256) {
-    sk[e / 128][e % 128] = k[(long long)p * Tk * 128 + e] * 0.25f;
-    sv[e / 128][e % 128] = v[(long long)p * Tk * 128 + e];
+  using namespace t2;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int p = blockIdx.x / nchunk, chunk = blockIdx.x - p * nchunk;
+  const int r0 = chunk * i2::CHUNK;
+  const int nstep = min(i2::CHUNK, L - r0) / STEP;
+  char* ring = tsm + hp * WAVE_LDS;
+  bf16x8 khi, klo, vop, vlo;
+  tok_op(k, p, Tk, hp, 0.25f * L2E, lane, khi, klo);
+  tok_op(v, p, Tk, hp, 1.0f, lane, vop, vlo);
+  s16x4 ak[2];
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) ak[hl] = tokT_op(k, p, Tk, hp, hl, 0.25f, lane);  // K_h^T / 4 [d = c][n = 4g+j]
+  bool nv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) nv[i] = ((4 * g + i) & 7) < Tk;
+  const bool cv = (c & 7) < Tk;
+  const bf16* qb = q + (long long)(p / q_rep) * L * ldq + hp * 32;
+  const bf16* db = dout + (long long)p * L * lddo + hp * 32;
+  f32x4 dka[2], dva[2];
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) dka[hl] = dva[hl] = (f32x4)0.0f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int s = 0; s < RING - 1 && s < nstep; ++s) load_step(qb, ldq, db, lddo, r0 + s * STEP, ring + s * STEP_BYTES, lane);
+  for (int s = 0; s < nstep; ++s) {
+    if (s + RING - 1 < nstep) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      load_step(qb, ldq, db, lddo, r0 + (s + RING - 1) * STEP, ring + ((s + RING - 1) % RING) * STEP_BYTES, lane);
+    }
+    // loads of steps s+1 .. s+3 and the 4 dq stores of each of the steps max(0, s-3) .. s-1 follow step s's loads
+    wait_vm(4 * min(RING - 1, nstep - 1 - s) + 4 * min(RING - 1, s));
+    const char* slot = ring + (s % RING) * STEP_BYTES;
+    const char* dimg = slot + 2048;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 qf = row_op(slot, t, false, lane), df = row_op(dimg, t, true, lane);
+      // transposed orientation [n 4g+i][r c]: softmax statistics and dQ
+      f32x4 sT = mfma32(khi, qf, (f32x4)0.0f);
+      sT = mfma32(klo, qf, sT);
+      const f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, sT[i]) : mx;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      f32x4 pT;
+      float sum = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pT[i] = nv[i] ? __builtin_amdgcn_exp2f(sT[i] - mx) : 0.0f;
+        sum += pT[i];
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      const float inv = 1.0f / sum;
+      float del = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pT[i] *= inv;
+        del = fmaf(pT[i], dpT[i], del);
+      }
+      del += __shfl_xor(del, 16, 64);
+      f32x4 dsT;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dsT[i] = pT[i] * (dpT[i] - del);
+      const s16x4 dsTb = pack4(dsT);
+      bf16* dqr = dq + ((long long)p * L + r0 + s * STEP + 16 * t + c) * lddq + hp * 32 + 4 * g;
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) *(s16x4*)(dqr + 16 * hl) = pack4(mfma16(ak[hl], dsTb, (f32x4)0.0f));
+      // untransposed [r 4g+i][n c] for dK / dV; row statistics from lane 32 h + r (h = head of column c)
+      f32x4 sS = mfma32(qf, khi, (f32x4)0.0f);
+      sS = mfma32(qf, klo, sS);
+      const f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+      f32x4 pS, dsS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int src = 32 * (c >> 3) + 4 * g + i;
+        const float Mi = __shfl(mx, src, 64), Ii = __shfl(inv, src, 64), Di = __shfl(del, src, 64);
+        pS[i] = cv ? __builtin_amdgcn_exp2f(sS[i] - Mi) * Ii : 0.0f;
+        dsS[i] = pS[i] * (dpS[i] - Di);
+      }
+      const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        dka[hl] = mfma16(tr_op(slot, t, hl, false, lane), dsSb, dka[hl]);  // dK^T[d 4g+i][n c] (x4)
+        dva[hl] = mfma16(tr_op(dimg, t, hl, true, lane), pSb, dva[hl]);   // dV^T[d 4g+i][n c]
+      }
+    }
   }
-  __syncthreads();
-  const int h = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const long long qb = (long long)(p / q_rep) * L;
-  // phase-2 ownership: 2*Tk*128 outputs over 256 threads
-  float accs[2 * MAXT * 128 / 256];
-#pragma unroll
-  for (int i = 0; i < 2 * MAXT * 128 / 256; ++i) accs[i] = 0.0f;
-  const int nout = 2 * Tk * 128;
-  for (int it = 0; it < I2T_ROWS / 32; ++it) {
-    const int r = r0 + it * 32 + rl;
-    const bool valid = r < L;
-    float qf[16], dof[16];
-    if (valid) {
-      const bf16* qr = q + (qb + r) * ldq + h * 16;
-      const bf16* dr = dout + ((long long)p * L + r) * lddo + h * 16;
-      bf16x8 a0 = *(const bf16x8*)qr, a1 = *(const bf16x8*)(qr + 8);
-      bf16x8 b0 = *(const bf16x8*)dr, b1 = *(const bf16x8*)(dr + 8);
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        qf[d] = (float)a0[d]; qf[8 + d] = (float)a1[d];
-        dof[d] = (float)b0[d]; dof[8 + d] = (float)b1[d];
-      }
-    } else {
-#pragma unroll
-      for (int d = 0; d < 16; ++d) { qf[d] = 0.0f; dof[d] = 0.0f; }
-    }
-    float s[MAXT], dp[MAXT];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) {
-        float acc = 0.0f, acc2 = 0.0f;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) { acc += qf[d] * sk[j][h * 16 + d]; acc2 += dof[d] * sv[j][h * 16 + d]; }
-        s[j] = acc;
-        dp[j] = acc2;
-        mx = fmaxf(mx, acc);
-      }
-    float sum = 0.0f;
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) { s[j] = __expf(s[j] - mx); sum += s[j]; }
-    const float inv = 1.0f / sum;
-    float dsum = 0.0f;
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) { s[j] *= inv; dsum += s[j] * dp[j]; }
-    float dqf[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) dqf[d] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < MAXT; ++j)
-      if (j < Tk) {
-        float ds = valid ? s[j] * (dp[j] - dsum) : 0.0f;
-        sds[rl][h][j] = ds;
-        spr[rl][h][j] = valid ? s[j] : 0.0f;
-#pragma unroll
-        for (int d = 0; d < 16; ++d) dqf[d] += ds * sk[j][h * 16 + d];  // sk already * 0.25
-      }
-    if (valid) {
-      bf16x8 o0, o1;
-#pragma unroll
-      for (int d = 0; d < 8; ++d) { o0[d] = (bf16)dqf[d]; o1[d] = (bf16)dqf[8 + d]; }
-      bf16* dr = dq + ((long long)p * L + r) * lddq + h * 16;
-      *(bf16x8*)dr = o0;
-      *(bf16x8*)(dr + 8) = o1;
-    }
-#pragma unroll
-    for (int d = 0; d < 16; ++d) { sq[rl][h * 16 + d] = qf[d]; sdo[rl][h * 16 + d] = dof[d]; }
-    __syncthreads();
-    // phase 2: dk[j][c] += 0.25 * sum_r ds[r][h(c)][j] * q[r][c];  dv[j][c] += sum_r p[r][h(c)][j] * dout[r][c]
-#pragma unroll
-    for (int i = 0; i < 2 * MAXT * 128 / 256; ++i) {
-      int o = threadIdx.x + i * 256;
-      if (o < nout) {
-        int which = o / (Tk * 128), jc = o % (Tk * 128), j = jc / 128, c = jc % 128, hh = c / 16;
-        float a = 0.0f;
-        if (which == 0) {
-          for (int rr = 0; rr < 32; ++rr) a += sds[rr][hh][j] * sq[rr][c];
-          a *= 0.25f;
-        } else {
-          for (int rr = 0; rr < 32; ++rr) a += spr[rr][hh][j] * sdo[rr][c];
-        }
-        accs[i] += a;
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 2 * MAXT * 128 / 256; ++i) {
-    int o = threadIdx.x + i * 256;
-    if (o < nout) part[((long long)blockIdx.x * P + p) * nout + o] = accs[i];
+  if (cv) {
+    const int hl = c >> 3, j = c & 7, h = 2 * hp + hl;
+    float* w = part + (((long long)chunk * P + p) * 2) * Tk * 128 + j * 128 + h * 16 + 4 * g;
+    *(f32x4*)w = (hl ? dka[1] : dka[0]) * 0.25f;
+    *(f32x4*)(w + Tk * 128) = hl ? dva[1] : dva[0];
   }
 }
 
@@ -442,55 +587,91 @@ extern "C" int octsam_dec_tok_attn_bwd(const float* q, const float* k, const flo
   return 0;
 }
 
+static int t2i_nchunk(int L) { return (L + t2::CHUNK - 1) / t2::CHUNK; }
+
+extern "C" int64_t octsam_dec_t2i_workspace(int32_t P, int32_t L) {
+  return (int64_t)P * t2i_nchunk(L) * 4 * t2::PART;
+}
+
+static void t2i_smem_attr() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)t2i_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM);
+    (void)hipFuncSetAttribute((const void*)t2i_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM);
+    done = true;
+  }
+}
+
 extern "C" int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
-                                  int32_t Tq, int32_t L, void* out, float* lse, void* stream) {
-  OCTSAM_CHECK_ARG(q && k && v && out && lse && P > 0 && Tq > 0 && Tq <= MAXT && L > 0 && kv_rep > 0 && ldkv % 8 == 0,
+                                  int32_t Tq, int32_t L, void* out, float* lse, float* workspace, void* stream) {
+  OCTSAM_CHECK_ARG(q && k && v && out && lse && workspace && P > 0 && Tq > 0 && Tq <= MAXT && L > 0 && L % 32 == 0 &&
+                       kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 && (uintptr_t)k % 16 == 0 &&
+                       (uintptr_t)v % 16 == 0,
                    "octsam_dec_t2i_fwd: bad args");
-  int nblk = ((P + 7) / 8) * 64;
-  hipLaunchKernelGGL(t2i_fwd_kernel, dim3(nblk), dim3(Tq * 64), 0, (hipStream_t)stream, q, (const bf16*)k,
-                     (const bf16*)v, ldkv, kv_rep, P, Tq, L, (bf16*)out, lse);
+  t2i_smem_attr();
+  const int nch = t2i_nchunk(L);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(t2i_fwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, s, q, (const bf16*)k, (const bf16*)v, ldkv,
+                     kv_rep, Tq, L, nch, workspace);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
+  hipLaunchKernelGGL(t2i_combine_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)out, lse);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
   return 0;
 }
 
 extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
                                   int32_t Tq, int32_t L, const void* out, const float* dout, const float* lse, void* dq,
-                                  void* dk, void* dv, int64_t lddkv, void* stream) {
-  OCTSAM_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv && P > 0 && Tq > 0 && Tq <= MAXT && L > 0 &&
-                       kv_rep > 0 && ldkv % 8 == 0 && lddkv % 8 == 0,
+                                  void* dk, void* dv, int64_t lddkv, float* workspace, void* stream) {
+  OCTSAM_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv && workspace && P > 0 && Tq > 0 &&
+                       Tq <= MAXT && L > 0 && L % 32 == 0 && kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 &&
+                       lddkv % 4 == 0 && (uintptr_t)k % 16 == 0 && (uintptr_t)v % 16 == 0 &&
+                       (uintptr_t)dk % 8 == 0 && (uintptr_t)dv % 8 == 0,
                    "octsam_dec_t2i_bwd: bad args");
-  int nblk = ((P + 7) / 8) * 64;
-  hipLaunchKernelGGL(t2i_bwd_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, q, (const bf16*)k, (const bf16*)v,
-                     ldkv, kv_rep, P, Tq, L, (const bf16*)out, dout, lse, (bf16*)dq, (bf16*)dk, (bf16*)dv, lddkv);
+  t2i_smem_attr();
+  const int nch = t2i_nchunk(L);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(t2i_bwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, s, q, (const bf16*)k, (const bf16*)v, ldkv,
+                     kv_rep, Tq, L, nch, (const bf16*)out, dout, lse, (bf16*)dk, (bf16*)dv, lddkv, workspace);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
+  hipLaunchKernelGGL(t2i_dq_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)dq);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
   return 0;
 }
 
+static int i2t_nchunk(int L) { return (L + i2::CHUNK - 1) / i2::CHUNK; }
+
 extern "C" int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P,
                                   int32_t Tk, int32_t L, void* out, int64_t ldo, void* stream) {
-  OCTSAM_CHECK_ARG(q && k && v && out && P > 0 && Tk > 0 && Tk <= MAXT && L > 0 && q_rep > 0 && ldq % 8 == 0 &&
-                       ldo % 8 == 0,
+  OCTSAM_CHECK_ARG(q && k && v && out && P > 0 && Tk > 0 && Tk <= MAXT && L > 0 && L % 16 == 0 && q_rep > 0 &&
+                       P % q_rep == 0 && ldq % 8 == 0 && ldo % 4 == 0 && (uintptr_t)q % 16 == 0 &&
+                       (uintptr_t)out % 8 == 0,
                    "octsam_dec_i2t_fwd: bad args");
-  dim3 grid((L + I2T_ROWS - 1) / I2T_ROWS, P);
-  hipLaunchKernelGGL(i2t_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, ldq, q_rep, k, v, Tk, L,
-                     (bf16*)out, ldo);
+  const int nch = i2t_nchunk(L);
+  hipLaunchKernelGGL(i2t_fwd_kernel, dim3(P * nch), dim3(256), 0, (hipStream_t)stream, (const bf16*)q, ldq, q_rep, k, v,
+                     Tk, L, nch, (bf16*)out, ldo);
   OCTSAM_LAUNCH_CHECK("octsam_dec_i2t_fwd");
   return 0;
 }
 
 extern "C" int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L) {
-  return (int64_t)((L + I2T_ROWS - 1) / I2T_ROWS) * P * 2 * Tk * 128;
+  return (int64_t)i2t_nchunk(L) * P * 2 * Tk * 128;
 }
 
 extern "C" int octsam_dec_i2t_bwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P,
                                   int32_t Tk, int32_t L, const void* dout, int64_t lddo, void* dq, int64_t lddq,
                                   float* partials, void* stream) {
-  OCTSAM_CHECK_ARG(q && k && v && dout && dq && partials && P > 0 && Tk > 0 && Tk <= MAXT && L > 0 && q_rep > 0 &&
-                       ldq % 8 == 0 && lddo % 8 == 0 && lddq % 8 == 0,
+  OCTSAM_CHECK_ARG(q && k && v && dout && dq && partials && P > 0 && Tk > 0 && Tk <= MAXT && L > 0 && L % 32 == 0 &&
+                       q_rep > 0 && P % q_rep == 0 && ldq % 8 == 0 && lddo % 8 == 0 && lddq % 4 == 0 &&
+                       (uintptr_t)q % 16 == 0 && (uintptr_t)dout % 16 == 0 && (uintptr_t)dq % 8 == 0,
                    "octsam_dec_i2t_bwd: bad args");
-  dim3 grid((L + I2T_ROWS - 1) / I2T_ROWS, P);
-  hipLaunchKernelGGL(i2t_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, ldq, q_rep, k, v, Tk, L,
-                     (const bf16*)dout, lddo, (bf16*)dq, lddq, partials, P);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)i2t_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, t2::SMEM);
+    attr = true;
+  }
+  const int nch = i2t_nchunk(L);
+  hipLaunchKernelGGL(i2t_bwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, (hipStream_t)stream, (const bf16*)q, ldq,
+                     q_rep, k, v, Tk, L, nch, (const bf16*)dout, lddo, (bf16*)dq, lddq, partials, P);
   OCTSAM_LAUNCH_CHECK("octsam_dec_i2t_bwd");
   return 0;
 }

@@ -186,13 +186,22 @@ def tok_attn_bwd(q, k, v, probs, dout, P, T, dq, dk, dv):
     _lib.call("octsam_dec_tok_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(probs), ptr(dout), P, T, ptr(dq), ptr(dk), ptr(dv))
 
 
+def _t2i_workspace(P, L, device):
+    n = _lib.load().octsam_dec_t2i_workspace(P, L)
+    return torch.empty(n, device=device, dtype=torch.float32)
+
+
 def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse):
-    _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse))
+    _require_cuda(q, k, v, out, lse)
+    ws = _t2i_workspace(P, L, q.device)
+    _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse), ptr(ws))
 
 
 def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
+    _require_cuda(q, k, v, out, dout, lse, dq, dk, dv)
+    ws = _t2i_workspace(P, L, q.device)
     _lib.call("octsam_dec_t2i_bwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(dout), ptr(lse),
-              ptr(dq), ptr(dk), ptr(dv), lddkv)
+              ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
 
 
 def i2t_fwd(q, ldq, q_rep, k, v, P, Tk, L, out, ldo):
@@ -202,7 +211,7 @@ def i2t_fwd(q, ldq, q_rep, k, v, P, Tk, L, out, ldo):
 def i2t_bwd(q, ldq, q_rep, k, v, P, Tk, L, dout, lddo, dq, lddq):
     """Returns dk, dv fp32 [P, Tk, 128] each."""
     n = _lib.load().octsam_dec_i2t_bwd_partials(P, Tk, L)
-    nb = (L + 255) // 256
+    nb = n // (P * 2 * Tk * 128)
     part = torch.empty(n, device=k.device, dtype=torch.float32)
     _lib.call("octsam_dec_i2t_bwd", ptr(q), ldq, q_rep, ptr(k), ptr(v), P, Tk, L, ptr(dout), lddo, ptr(dq), lddq,
               ptr(part))

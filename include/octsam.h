@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 2
+#define OCTSAM_ABI_VERSION 3
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -167,19 +167,22 @@ int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
  * tok: q,k,v fp32 [P,T,256] (8 heads x 32) -> out bf16; probs fp32 [P,8,T,T] saved for backward.
  * t2i: q fp32 [P,Tq,128] (8 heads x 16); k,v bf16 rows of [.., L, ldkv], block p/kv_rep
  *      (kv_rep = prompts per image when K/V are per image); out bf16 [P,Tq,128]; lse fp32 [P,8,Tq].
- *      backward writes dq bf16 [P,Tq,128] and per-prompt dk, dv bf16 [P, L, lddkv].
+ *      backward writes dq bf16 [P,Tq,128] and per-prompt dk, dv bf16 [P, L, lddkv]. Both take a caller-owned
+ *      fp32 workspace of octsam_dec_t2i_workspace(P, L) elements (per-chunk partials); L % 32 == 0,
+ *      k, v 16-B aligned, ldkv % 8 == 0, lddkv % 4 == 0.
  * i2t: q bf16 rows of [.., L, ldq], block p/q_rep; k,v fp32 [P,Tk,128]; out bf16 [P, L, ldo].
- *      backward writes dq bf16 [P, L, lddq] and partials fp32 [L/256, P, 2, Tk, 128] (dk; dv),
+ *      backward writes dq bf16 [P, L, lddq] and partials fp32 [ceil(L/512), P, 2, Tk, 128] (dk; dv),
  *      reduce with octsam_splitk_reduce; octsam_dec_i2t_bwd_partials() gives the element count. */
 int octsam_dec_tok_attn_fwd(const float* q, const float* k, const float* v, int32_t P, int32_t T, void* out,
                             float* probs, void* stream);
 int octsam_dec_tok_attn_bwd(const float* q, const float* k, const float* v, const float* probs, const float* dout,
                             int32_t P, int32_t T, void* dq, void* dk, void* dv, void* stream);
+int64_t octsam_dec_t2i_workspace(int32_t P, int32_t L);
 int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
-                       int32_t L, void* out, float* lse, void* stream);
+                       int32_t L, void* out, float* lse, float* workspace, void* stream);
 int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
                        int32_t L, const void* out, const float* dout, const float* lse, void* dq, void* dk, void* dv,
-                       int64_t lddkv, void* stream);
+                       int64_t lddkv, float* workspace, void* stream);
 int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
                        int32_t L, void* out, int64_t ldo, void* stream);
 int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L);

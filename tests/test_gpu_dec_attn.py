@@ -1,0 +1,118 @@
+"""Mask-decoder attention cores (SamAttention core, hf:modeling_sam.py:231-270, in the three shapes of
+SamTwoWayTransformer :273-405) vs plain PyTorch fp32 references of the same op on the same bf16-rounded
+inputs: token->image (t2i, 7 queries x 4096 keys, 8 heads x 16, K/V optionally shared per image) and
+image->token (i2t, 4096 queries x 7 keys), forward and backward.
+
+Tolerances: outputs and gradients are bf16 (rel. rounding 2^-9) and the kernels take the token-side
+operands through bf16 MFMAs (queries split hi+lo), so max-abs errors are bounded at 2e-2 of the
+tensor's max magnitude, and the forward log-sum-exp at 1e-3 absolute."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+L, CI, H, DH = 4096, 128, 8, 16
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+def _heads(x):  # [..., 128] -> [..., 8, 16]
+    return x.reshape(*x.shape[:-1], H, DH)
+
+
+def _t2i_ref(q, k, v, kv_rep):
+    """q [P,T,128] fp32; k, v [B, L, 128] fp32 (B = P / kv_rep) -> out [P,T,128], lse [P,8,T]."""
+    P = q.shape[0]
+    kk = k.repeat_interleave(kv_rep, 0)
+    vv = v.repeat_interleave(kv_rep, 0)
+    s = torch.einsum("pthd,plhd->phtl", _heads(q), _heads(kk)) * 0.25
+    lse = torch.logsumexp(s, -1)
+    o = torch.einsum("phtl,plhd->pthd", s.softmax(-1), _heads(vv)).reshape(P, -1, CI)
+    return o, lse
+
+
+@pytest.mark.parametrize("P,kv_rep,T,ld", [(6, 1, 7, 384), (6, 3, 7, 384), (5, 1, 5, 256)])
+def test_t2i_fwd_bwd(cuda, P, kv_rep, T, ld):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(P * 10 + kv_rep + T)
+    B = P // kv_rep
+    buf = (torch.randn(B * L, ld, generator=g) * 1.5).to(cuda, torch.bfloat16)
+    vcol = ld - CI
+    kb, vb = buf[:, :CI], buf[:, vcol:]
+    q = (torch.randn(P, T, CI, generator=g) * 2).to(cuda)
+    out = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(P, H, T, device=cuda)
+    kernels.t2i_fwd(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, lse)
+    qr = q.clone().requires_grad_()
+    kr = kb.float().reshape(B, L, CI).requires_grad_()
+    vr = vb.float().reshape(B, L, CI).requires_grad_()
+    oref, lref = _t2i_ref(qr, kr, vr, kv_rep)
+    assert _rel(out, oref) < 2e-2
+    assert (lse - lref).abs().max().item() < 1e-3
+    # backward: per-prompt dK, dV (summed over an image's prompts by the caller), dq
+    dout = torch.randn(P, T, CI, generator=g).to(cuda)
+    oref.backward(dout)
+    dkv = torch.empty(P * L, 2 * CI, device=cuda, dtype=torch.bfloat16)
+    dq = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+    kernels.t2i_bwd(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, dout, lse, dq, dkv, dkv[:, CI:], 2 * CI)
+    dk = dkv[:, :CI].float().reshape(B, kv_rep, L, CI).sum(1)
+    dv = dkv[:, CI:].float().reshape(B, kv_rep, L, CI).sum(1)
+    assert _rel(dq, qr.grad) < 2e-2
+    assert _rel(dk, kr.grad) < 2e-2
+    assert _rel(dv, vr.grad) < 2e-2
+
+
+def _i2t_ref(qimg, k, v, q_rep):
+    """qimg [B, L, 128]; k, v [P, T, 128] -> out [P, L, 128]."""
+    qq = qimg.repeat_interleave(q_rep, 0)
+    s = torch.einsum("plhd,pthd->phlt", _heads(qq), _heads(k)) * 0.25
+    return torch.einsum("phlt,pthd->plhd", s.softmax(-1), _heads(v)).reshape(qq.shape[0], L, CI)
+
+
+@pytest.mark.parametrize("P,q_rep,T,ldq", [(6, 1, 7, 384), (6, 3, 7, 128), (4, 2, 4, 384)])
+def test_i2t_fwd_bwd(cuda, P, q_rep, T, ldq):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(P * 7 + q_rep + T)
+    B = P // q_rep
+    qbuf = (torch.randn(B * L, ldq, generator=g) * 1.5).to(cuda, torch.bfloat16)
+    qv = qbuf[:, :CI]
+    k = (torch.randn(P, T, CI, generator=g) * 2).to(cuda)
+    v = torch.randn(P, T, CI, generator=g).to(cuda)
+    out = torch.empty(P * L, CI, device=cuda, dtype=torch.bfloat16)
+    kernels.i2t_fwd(qbuf, ldq, q_rep, k, v, P, T, L, out, CI)
+    qr = qv.float().reshape(B, L, CI).requires_grad_()
+    kr = k.clone().requires_grad_()
+    vr = v.clone().requires_grad_()
+    oref = _i2t_ref(qr, kr, vr, q_rep)
+    assert _rel(out.view(P, L, CI), oref) < 2e-2
+    dout = torch.randn(P, L, CI, generator=g).to(cuda, torch.bfloat16)
+    oref.backward(dout.float())
+    dq = torch.empty(P * L, CI, device=cuda, dtype=torch.bfloat16)
+    dk, dv = kernels.i2t_bwd(qbuf, ldq, q_rep, k, v, P, T, L, dout, CI, dq, CI)
+    dqi = dq.float().reshape(B, q_rep, L, CI).sum(1)
+    assert _rel(dqi, qr.grad) < 2e-2
+    assert _rel(dk, kr.grad) < 2e-2
+    assert _rel(dv, vr.grad) < 2e-2
+
+
+def test_t2i_deterministic(cuda):
+    """Fixed-order reductions: two runs give identical bits."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(3)
+    P, T = 4, 7
+    buf = torch.randn(P * L, 384, generator=g).to(cuda, torch.bfloat16)
+    q = torch.randn(P, T, CI, generator=g).to(cuda)
+    dout = torch.randn(P, T, CI, generator=g).to(cuda)
+    res = []
+    for _ in range(2):
+        out = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+        lse = torch.empty(P, H, T, device=cuda)
+        kernels.t2i_fwd(q, buf, buf[:, 256:], 384, 1, P, T, L, out, lse)
+        dkv = torch.empty(P * L, 2 * CI, device=cuda, dtype=torch.bfloat16)
+        dq = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+        kernels.t2i_bwd(q, buf, buf[:, 256:], 384, 1, P, T, L, out, dout, lse, dq, dkv, dkv[:, CI:], 2 * CI)
+        res.append((out, lse, dq, dkv))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
