@@ -529,7 +529,7 @@ class MaskDecoder(nn.Module):
         s.up2, s.up2pre = up2, up2pre
         masks = torch.empty(P, nsel, 256, 256, device=dev, dtype=f32)
         K.mask_dot_fwd(up2, hyper, P, nsel, masks)
-        iou_sel = iou[:, sel].contiguous()
+        iou_sel = iou[:, sel[0]:sel[-1] + 1].contiguous()  # sel is a contiguous range (slice: capturable)
         return masks.view(B, N, nsel, 256, 256), iou_sel.view(B, N, nsel), s
 
     # ------------------------------------------------------------------ backward

@@ -210,30 +210,42 @@ def topo_entries(B: int, N: int, mode: str = "first", global_batch: int | None =
     return [[b * N] for b in range(B)]
 
 
-def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch.Tensor | None, *, lamda=0.1,
-                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=1024, logits=True,
-                          global_batch: int | None = None):
-    """Topological loss value (float) and, when dmask is given, its gradient added into dmask.
-    masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64)."""
-    if lamda == 0.0:
-        return 0.0
+_TOPO_INDEX: dict = {}
+
+
+def topo_index(B: int, N: int, mode: str, global_batch: int | None, device):
+    """(entries, maps, device int32 map index) of the topological loss for a [B, N] mask batch (cached: the
+    index tensor's address stays fixed, so captured graphs may read it)."""
+    key = (B, N, mode, global_batch, str(device))
+    if key not in _TOPO_INDEX:
+        entries = topo_entries(B, N, mode, global_batch)
+        maps = sorted({m for e in entries for m in e})
+        midx = torch.tensor(maps, dtype=torch.int32, device=device) if maps else None
+        _TOPO_INDEX[key] = (entries, maps, midx)
+    return _TOPO_INDEX[key]
+
+
+def topo_device_forward(masks: torch.Tensor, gt_u8: torch.Tensor, midx: torch.Tensor, *, interp=50, feat_d=1,
+                        max_pairs=1024, logits=True):
+    """Device half of the topological loss forward (no host sync; capturable): 50x50 align-corners
+    resampling of sigmoid(pred) and gt (topological_loss.py:33-46) and cubical persistence of both
+    (:55-63). Returns (pairs [2Kn, max_pairs, 2] of dim feat_d, counts [2Kn, 3], maps [2Kn, interp^2])."""
     B, N, H, W = masks.shape
+    Kn = midx.numel()
     dev = masks.device
-    entries = topo_entries(B, N, mode, global_batch)
-    if not entries:
-        return 0.0
-    maps = sorted({m for e in entries for m in e})
-    Kn = len(maps)
-    midx = torch.tensor(maps, dtype=torch.int32, device=dev)
-    pred = torch.empty(Kn, interp, interp, device=dev, dtype=torch.float32)
-    gt50 = torch.empty(Kn, interp, interp, device=dev, dtype=torch.float32)
+    both = torch.empty(2 * Kn, interp, interp, device=dev, dtype=torch.float32)
     _lib.call("octsam_topo_down", K.ptr(masks), K.ptr(gt_u8), K.ptr(midx), Kn, H, W, interp, interp, int(logits),
-              K.ptr(pred), K.ptr(gt50))
-    both = torch.cat([pred, gt50], 0)
+              K.ptr(both[:Kn]), K.ptr(both[Kn:]))
     p0, p1, ess, cnt = K.cubical_ph(both, max_pairs=max_pairs)
-    pairs = (p0 if feat_d == 0 else p1)
-    host = [t.cpu() for t in (pairs, cnt, both)]  # one D2H sync per step (diagrams are tiny)
-    pairs_h, cnt_h, vals_h = host[0].numpy(), host[1].numpy(), host[2].numpy().reshape(2 * Kn, -1)
+    return (p0 if feat_d == 0 else p1), cnt, both.view(2 * Kn, interp * interp)
+
+
+def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entries, maps, *, lamda=0.1, feat_d=1,
+              loss_q=2, want_grad=True):
+    """Host half: W2 between the H_feat_d diagrams of pred and gt per loss entry (topological_loss.py:68-96,
+    torch_topological WassersteinDistance(q) -> exact OT, restated in octsam_w2_host). Returns the loss
+    (float) and d loss / d pred-map values [Kn, interp^2] (float32; None without want_grad)."""
+    Kn = len(maps)
     if cnt_h[:, 2].any():
         raise RuntimeError("persistence pair buffer overflow; raise max_pairs")
     col = 0 if feat_d == 0 else 1
@@ -245,7 +257,7 @@ def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch
         return np.stack([v[pr[:, 0]], v[pr[:, 1]]], 1) if n else np.zeros((0, 2), np.float32), pr
 
     pos = {m: i for i, m in enumerate(maps)}
-    dpred = np.zeros((Kn, interp * interp), np.float32)
+    dpred = np.zeros((Kn, vals_h.shape[1]), np.float32) if want_grad else None
     total = 0.0
     for e in entries:
         costs, grads = [], []
@@ -259,7 +271,7 @@ def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch
         tot = float(np.float32(sum(costs)))
         w = tot ** (1.0 / loss_q)
         total += w
-        if dmask is not None:
+        if want_grad:
             # d(tot^(1/q)) / d tot  (inf * 0 -> nan at tot == 0, as torch's pow backward would give)
             dd = (1.0 / loss_q) * (tot ** (1.0 / loss_q - 1.0)) if tot > 0 else float("inf")
             for k, pr1, g in grads:
@@ -268,11 +280,36 @@ def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch
                 scale = lamda / len(entries) * dd
                 np.add.at(dpred[k], pr1[:, 0], (scale * g[:, 0]).astype(np.float32))
                 np.add.at(dpred[k], pr1[:, 1], (scale * g[:, 1]).astype(np.float32))
-    loss = lamda * total / len(entries)
+    return lamda * total / len(entries), dpred
+
+
+def topo_device_backward(masks: torch.Tensor, midx: torch.Tensor, dp: torch.Tensor, dmask: torch.Tensor, *,
+                         interp=50, logits=True):
+    """dmask += d topo / d masks, given d topo / d (resampled sigmoid map) dp [Kn, interp^2] (capturable)."""
+    B, N, H, W = masks.shape
+    _lib.call("octsam_topo_bwd", K.ptr(masks), K.ptr(midx), midx.numel(), H, W, interp, interp, int(logits),
+              K.ptr(dp), 1.0, K.ptr(dmask))
+
+
+def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch.Tensor | None, *, lamda=0.1,
+                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=1024, logits=True,
+                          global_batch: int | None = None):
+    """Topological loss value (float) and, when dmask is given, its gradient added into dmask.
+    masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64)."""
+    if lamda == 0.0:
+        return 0.0
+    B, N, H, W = masks.shape
+    entries, maps, midx = topo_index(B, N, mode, global_batch, masks.device)
+    if not entries:
+        return 0.0
+    pairs, cnt, both = topo_device_forward(masks, gt_u8, midx, interp=interp, feat_d=feat_d, max_pairs=max_pairs,
+                                           logits=logits)
+    host = [t.cpu() for t in (pairs, cnt, both)]  # one D2H sync per step (diagrams are tiny)
+    loss, dpred = topo_host(host[0].numpy(), host[1].numpy(), host[2].numpy(), entries, maps, lamda=lamda,
+                            feat_d=feat_d, loss_q=loss_q, want_grad=dmask is not None)
     if dmask is not None:
-        dp = torch.from_numpy(dpred).to(dev)
-        _lib.call("octsam_topo_bwd", K.ptr(masks), K.ptr(midx), Kn, H, W, interp, interp, int(logits), K.ptr(dp), 1.0,
-                  K.ptr(dmask))
+        topo_device_backward(masks, midx, torch.from_numpy(dpred).to(masks.device), dmask, interp=interp,
+                             logits=logits)
     return loss
 
 

@@ -19,14 +19,34 @@ import time
 import torch
 
 from . import kernels as K
-from .losses import dicece_forward_backward, postproc_backward, postproc_forward, topo_forward_backward
+from .losses import (dicece_forward_backward, postproc_backward, postproc_forward, topo_device_backward,
+                     topo_device_forward, topo_host, topo_index)
 from .model import SamModel
 
 
+class _Phases:
+    """Tensors that flow between the phases of one step (static across graph replays)."""
+
+
 class FusedTrainStep:
+    """One training step of the reference (training_utils.py:46-69) as three phases:
+
+      E  encoder forward + prompt tokens              (reads no trainable weight)
+      F  decoder forward, post-processing, DiceCE fwd/bwd, topo-loss device forward (PH), D2H of the
+         persistence pairs
+      -- host: W2 between diagrams (POT emd2 restated) -> d topo / d map, topo loss
+      B  H2D of the topo gradient, topo backward, post-processing backward, decoder backward
+      then (world > 1) the RCCL all-reduce of the flat decoder gradient and Adam.
+
+    graphs=True captures E, F and B as hipGraphs (one pool, replayed in capture order) the first time a
+    batch shape is seen, after eager warm-up, and replays them afterwards: no per-kernel host launch cost.
+    In data-parallel runs (overlap=True) the all-reduce runs on a side stream and Adam is deferred to the
+    next step, after that step's encoder forward has been queued: the gradient exchange overlaps the
+    encoder; flush() completes a pending update."""
+
     def __init__(self, model: SamModel, lr: float = 1e-3, weight_decay: float = 0.0, topological: bool = False,
                  lamda: float = 0.1, interp: int = 50, betas=(0.9, 0.999), eps: float = 1e-8,
-                 topo_mode: str = "first", process_group=None):
+                 topo_mode: str = "first", process_group=None, graphs: bool = False, overlap: bool = True):
         self.model = model
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.topological, self.lamda, self.interp, self.topo_mode = topological, lamda, interp, topo_mode
@@ -36,6 +56,11 @@ class FusedTrainStep:
         self.t = 0
         self.pg = process_group
         self._pe = None
+        self.graphs = graphs
+        self.overlap = overlap and process_group is not None
+        self._g = None          # captured graphs + static tensors for one batch shape
+        self._pending = None    # (event, ) of an all-reduce whose Adam step has not run yet
+        self._side = None
 
     def image_pe(self):
         G = self.model.shared_image_embedding.positional_embedding
@@ -44,37 +69,162 @@ class FusedTrainStep:
             self._pe = (tag, self.model.image_pe())
         return self._pe[1]
 
+    # ------------------------------------------------------------------ phases
+    def _phase_e(self, st):
+        st.emb = self.model.vision_encoder.forward_nhwc(st.pixel_values)
+        st.tokens = self.model.prompt_tokens(st.input_points, st.input_labels, st.input_boxes)
+
+    def _phase_f(self, st, backward):
+        model = self.model
+        dec = model.mask_decoder
+        B, N = st.tokens.shape[:2]
+        H, W = st.orig
+        low, _, st.saved = dec.forward_impl(st.emb, self.image_pe(), st.tokens,
+                                            model.prompt_encoder.no_mask_embed.weight.detach(), False)
+        gt = st.gt_u8.reshape(B * N, H, W)
+        masks, dpart = postproc_forward(low.view(B * N, 256, 256), st.crop, st.orig, gt)
+        st.masks = masks.view(B, N, H, W)
+        st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), dpart)
+        st.topo_dev = None
+        if self.topological and self.lamda != 0.0:
+            entries, maps, midx = topo_index(B, N, self.topo_mode, st.global_batch, masks.device)
+            if entries:
+                pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
+                st.topo_dev = (entries, maps, midx)
+                if st.pinned is not None:  # graph mode: async copies into fixed pinned buffers
+                    for h, d in zip(st.pinned, (pairs, cnt, vals)):
+                        h.copy_(d, non_blocking=True)
+                else:
+                    st.topo_out = (pairs, cnt, vals)
+
+    def _topo_host(self, st, backward):
+        """-> topo loss (float); in backward mode also fills the device (eager) / pinned (graph) gradient."""
+        if st.topo_dev is None:
+            return 0.0
+        entries, maps, midx = st.topo_dev
+        if st.pinned is not None:
+            pairs_h, cnt_h, vals_h = (t.numpy() for t in st.pinned)
+        else:
+            pairs_h, cnt_h, vals_h = (t.cpu().numpy() for t in st.topo_out)
+        loss, dpred = topo_host(pairs_h, cnt_h, vals_h, entries, maps, lamda=self.lamda, feat_d=1, loss_q=2,
+                                want_grad=backward)
+        if backward:
+            if st.pinned is not None:
+                st.dp_pinned.numpy()[...] = dpred
+            else:
+                st.dp = torch.from_numpy(dpred).to(st.masks.device)
+        return loss
+
+    def _phase_b(self, st, backward):
+        B, N, H, W = st.masks.shape
+        if backward:
+            if st.topo_dev is not None:
+                if st.pinned is not None:
+                    st.dp.copy_(st.dp_pinned, non_blocking=True)
+                topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dmask, interp=self.interp)
+            dlow = postproc_backward(st.dmask.view(B * N, H, W), 256, st.crop, st.orig)
+            self.model.mask_decoder.backward_impl(st.saved, dlow.view(B, N, 1, 256, 256))
+        loss = st.loss_out
+        loss[0:2] = st.loss3[0:2]
+        if st.pinned is not None:
+            loss[2:3].copy_(st.topo_pinned, non_blocking=True)
+        else:
+            loss[2] = st.topo_val
+        loss[3] = st.loss3[2] + loss[2]
+
+    # ------------------------------------------------------------------ eager / graph drivers
+    def _state(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch):
+        st = _Phases()
+        st.pixel_values, st.gt_u8 = pixel_values, gt_u8
+        st.input_boxes, st.input_points, st.input_labels = input_boxes, input_points, input_labels
+        st.crop, st.orig, st.global_batch = tuple(crop), tuple(orig), global_batch
+        st.pinned = None
+        st.loss_out = torch.empty(4, device=pixel_values.device, dtype=torch.float64)
+        return st
+
     @torch.no_grad()
     def forward_backward(self, pixel_values, gt_u8, input_boxes=None, input_points=None, input_labels=None,
                          crop=(992, 1024), orig=(496, 512), global_batch=None, backward=True):
         """Returns a device float64 tensor [4] = (dice, ce, topo, total). With backward=True leaves the
         decoder gradient in mask_decoder.flat_grad. global_batch: images in the global (all-rank) batch,
         which fixes the topological loss's batch nesting."""
-        model = self.model
-        dec = model.mask_decoder
-        emb = model.vision_encoder.forward_nhwc(pixel_values)
-        tokens = model.prompt_tokens(input_points, input_labels, input_boxes)
-        B, N = tokens.shape[:2]
-        H, W = orig
-        low, _, saved = dec.forward_impl(emb, self.image_pe(), tokens,
-                                         model.prompt_encoder.no_mask_embed.weight.detach(), False)
-        gt = gt_u8.reshape(B * N, H, W)
-        masks, dpart = postproc_forward(low.view(B * N, 256, 256), crop, orig, gt)
-        masks = masks.view(B, N, H, W)
-        loss3, dmask = dicece_forward_backward(masks, gt_u8.view(B, N, H, W), dpart)
-        topo = 0.0
-        if self.topological:
-            topo = topo_forward_backward(masks, gt_u8.view(B, N, H, W), dmask if backward else None,
-                                         lamda=self.lamda, interp=self.interp, feat_d=1, loss_q=2,
-                                         mode=self.topo_mode, global_batch=global_batch)
-        if backward:
-            dlow = postproc_backward(dmask.view(B * N, H, W), 256, crop, orig)
-            dec.backward_impl(saved, dlow.view(B, N, 1, 256, 256))
-        loss = torch.empty(4, device=loss3.device, dtype=torch.float64)
-        loss[0:2] = loss3[0:2]
-        loss[2] = topo
-        loss[3] = loss3[2] + topo
-        return loss
+        if self.graphs and backward:
+            return self._graph_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop,
+                                                orig, global_batch)
+        return self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                                            global_batch, backward)
+
+    def _eager_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                                global_batch, backward):
+        st = self._state(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch)
+        self._phase_e(st)
+        self._finish_pending()
+        self._phase_f(st, backward)
+        st.topo_val = self._topo_host(st, backward)
+        self._phase_b(st, backward)
+        return st.loss_out
+
+    def _graph_key(self, *ts):
+        return tuple((None if t is None else (tuple(t.shape), t.dtype, t.data_ptr())) for t in ts)
+
+    def _capture(self, key, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch):
+        dev = pixel_values.device
+        self._g = None
+        # one eager pass first: lazily built operand caches, tables and kernel attributes exist before capture
+        self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                                     global_batch, True)
+        torch.cuda.synchronize()
+        st = self._state(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch)
+        B, N = gt_u8.shape[:2]
+        if self.topological and self.lamda != 0.0:
+            entries, maps, midx = topo_index(B, N, self.topo_mode, global_batch, dev)
+            Kn = len(maps)
+            if Kn:
+                st.pinned = (torch.empty((2 * Kn, 1024, 2), dtype=torch.int32, pin_memory=True),
+                             torch.empty((2 * Kn, 3), dtype=torch.int32, pin_memory=True),
+                             torch.empty((2 * Kn, self.interp * self.interp), dtype=torch.float32, pin_memory=True))
+                st.dp_pinned = torch.zeros((Kn, self.interp * self.interp), dtype=torch.float32, pin_memory=True)
+                st.dp = torch.zeros((Kn, self.interp * self.interp), dtype=torch.float32, device=dev)
+        if st.pinned is None:  # no host phase: the pinned topo scalar stays 0
+            st.pinned = ()
+        st.topo_pinned = torch.zeros(1, dtype=torch.float64, pin_memory=True)
+        ge, gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(ge, stream=s, capture_error_mode="relaxed"):
+                self._phase_e(st)
+            pool = ge.pool()
+            with torch.cuda.graph(gf, stream=s, pool=pool, capture_error_mode="relaxed"):
+                self._phase_f(st, True)
+            with torch.cuda.graph(gb, stream=s, pool=pool, capture_error_mode="relaxed"):
+                self._phase_b(st, True)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        if st.pinned == ():
+            st.pinned = None
+            st.topo_dev = None
+        self._g = (key, ge, gf, gb, st, torch.cuda.Event())
+
+    def _graph_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                                global_batch):
+        key = self._graph_key(pixel_values, gt_u8, input_boxes, input_points, input_labels) + (
+            tuple(crop), tuple(orig), global_batch)
+        if self._g is None or self._g[0] != key:
+            self._capture(key, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                          global_batch)
+        _, ge, gf, gb, st, ev = self._g
+        ge.replay()
+        self._finish_pending()
+        gf.replay()
+        if st.pinned is not None:
+            ev.record()
+            ev.synchronize()  # the persistence pairs are in the pinned buffers
+        loss = self._topo_host(st, True) if st.pinned is not None else 0.0
+        if st.pinned is not None:
+            st.topo_pinned.numpy()[0] = loss
+        gb.replay()
+        return st.loss_out
 
     @torch.no_grad()
     def allreduce_grads(self, n_local=None, n_global=None):
@@ -95,6 +245,35 @@ class FusedTrainStep:
         K.adam(dec.flat, dec.flat_grad, self.exp_avg, self.exp_avg_sq, beta1=b1, beta2=b2, eps=self.eps,
                weight_decay=self.wd, step_size=self.lr / bc1, bc2_sqrt=math.sqrt(bc2), params_bf16=dec.flat_b16)
 
+    def _launch_update(self, n_local, n_global):
+        """All-reduce (side stream when overlapping) then Adam, now or at the next _finish_pending."""
+        if self.pg is None or not self.overlap:
+            self.allreduce_grads(n_local, n_global)
+            self.optimizer_step()
+            return
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=main.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            self.allreduce_grads(n_local, n_global)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        self._pending = done
+
+    def _finish_pending(self):
+        if self._pending is None:
+            return
+        torch.cuda.current_stream().wait_event(self._pending)
+        self._pending = None
+        self.optimizer_step()
+
+    def flush(self):
+        """Apply a deferred (overlapped) parameter update."""
+        self._finish_pending()
+
     def step(self, batch: dict, n_global=None):
         """batch: device tensors from data.process_batch/to_device_batch. n_global: images in the global
         batch (data parallel; None = this rank's batch is the whole batch)."""
@@ -104,8 +283,7 @@ class FusedTrainStep:
         loss = self.forward_backward(batch["pixel_values"], batch["gt_u8"], input_boxes=batch.get("input_boxes"),
                                      input_points=batch.get("input_points"), input_labels=batch.get("input_labels"),
                                      crop=crop, orig=orig, global_batch=n_global)
-        self.allreduce_grads(n_local, n_global)
-        self.optimizer_step()
+        self._launch_update(n_local, n_global)
         return loss
 
 
@@ -282,9 +460,9 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
             else:  # nothing on this rank in a ragged last batch: contribute zero gradient
                 model.mask_decoder.flat_grad.zero_()
                 lv = torch.zeros((), dtype=torch.float64)
-            step.allreduce_grads(len(idx), n_glob)
-            step.optimizer_step()
+            step._launch_update(len(idx), n_glob)  # all-reduce (overlapped with the next encoder forward) + Adam
             epoch_loss += float(_collective_sum(lv.reshape(1), pg)[0]) / n_glob  # the .item() of :69
+        step.flush()
         epoch_loss /= len(batches)
         vloss = validate_model(step, vds, processor, bs, config, world, rank, pg, device)
         hist["train_loss"].append(epoch_loss)
