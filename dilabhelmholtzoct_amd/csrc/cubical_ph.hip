@@ -4,28 +4,36 @@
 // .persistence() + .cofaces_of_persistence_pairs() (ref:octsam/models/topological_loss.py:55-63).
 // Bit-exact target: oracle/cubical_ph.c (same total order, same coface rule, same pair order).
 //
-// Per map:
-//   1. pixels -> LDS; edge keys (ordered value bits << 32 | bitmap position) built in parallel and
-//      bitonic-sorted in LDS (gudhi's is_before_in_filtration among 1-cells).
-//   2. wave 0: H1 as the Alexander-dual union-find over pixels + exterior, edges in DECREASING
-//      order; wave 1: H0 union-find over vertices, edges in INCREASING order. Both run the elder
-//      rule in 64-edge chunks: every lane finds the roots of its own edge against the state at the
-//      chunk start (parallel, path halving), then a wave-uniform loop over the 64 edges resolves
-//      the merges in order with v_readlane broadcasts and whole-wave relabelling, so each edge costs
-//      a few scalar/VALU ops instead of a chain of dependent LDS round trips. The chunk's links are
-//      written back to the LDS forest after the loop.
-//   3. essential H0 class + argmax (torch_topological's fake destroyer), top-dimensional cofaces,
-//      pairs ranked by (persistence desc, destroyer filtration order) and written out.
+// Per map (one 512-thread workgroup, everything in LDS):
+//   1. node filtration order: vertices (lower-star value, bitmap position) and pixels (value, index) in
+//      one bitonic sort; nodes are renumbered by rank, so "younger" is an integer comparison.
+//   2. edge (1-cell) order: (lower-star value, bitmap position) -- gudhi's is_before_in_filtration among
+//      1-cells -- bitonic sort (every thread issues all its compare-exchange loads of a stage at once).
+//   3. wave 0: H1 as the Alexander-dual union-find over pixels + exterior, edges in DECREASING order;
+//      wave 1: H0 union-find over vertices, edges in INCREASING order. Elder rule in 64-edge chunks:
+//      lanes find their edge's roots against the chunk-start forest in parallel; a wave-uniform loop
+//      resolves the chunk's edges in order (two v_readlane, min/max, whole-wave relabel, lane-j select);
+//      merges are logged with ballot compaction.
+//   4. in parallel: positive-persistence merges -> pairs, essential H0 class + argmax (torch_topological's
+//      fake destroyer), top-dimensional cofaces, pairs ranked by (persistence desc, destroyer order).
 #include "common.h"
 #include "../../include/octsam.h"
 
 namespace {
 
+#ifdef PH_PROFILE  // phase timestamps (scripts/micro/ph_timing.hip only)
+__device__ unsigned long long g_ph_stamp[64];
+#define PH_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_ph_stamp[k] = __builtin_readcyclecounter()
+#define PH_STAMP_W(k) \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_ph_stamp[k] = __builtin_readcyclecounter()
+#else
+#define PH_STAMP(k)
+#define PH_STAMP_W(k)
+#endif
+
 constexpr int NTHR = 512;
 constexpr int MAX_PIX = 4096;
-constexpr int MAX_EDGES_POW2 = 8192;
-constexpr int MAX_VERT = 4225;  // (64+1)^2
-constexpr int REC_CAP = 1024;
 
 struct Map {
   int H, W, W2, H2;
@@ -78,163 +86,146 @@ __device__ int top_coface(const Map& m, int p) {
   return -1;
 }
 
-__device__ __forceinline__ int uf_find(int* parent, int a) {
+typedef uint16_t u16;
+
+__device__ __forceinline__ int uf_find(u16* parent, int a) {
   int p = parent[a];
   while (p != a) {
     int gp = parent[p];
-    parent[a] = gp;  // path halving; concurrent writers only ever store an ancestor
+    parent[a] = (u16)gp;  // path halving; concurrent writers only ever store an ancestor
     a = gp;
     p = parent[a];
   }
   return a;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
+constexpr int NP2 = 8192;        // sort width (edges; vertices + pixels)
+constexpr int MAXN = 4352;       // node arrays (vertices, pixels + exterior), u16
+constexpr int REC_CAP = 1024;
 
 struct Smem {
-  uint64_t keys[MAX_EDGES_POW2];
+  uint64_t keys[NP2];  // sort buffer; after the edge sort: epos u32[NP2] | merge logs u32[nv] | u32[npix]
   float vals[MAX_PIX];
-  int vpar[MAX_VERT];
-  int ppar[MAX_PIX + 1];
-  uint64_t rec_key[2][REC_CAP];
-  int rec_c[2][REC_CAP];
-  int nrec[2];
+  union {
+    struct {
+      u16 par[2][MAXN];  // union-find forests over filtration ranks: [0] vertices (H0), [1] pixels + ext (H1)
+      u16 vrank[MAXN];   // vertex id -> rank
+      u16 prank[MAXN];   // pixel -> rank
+    } uf;
+    struct {
+      uint64_t key[2][REC_CAP];  // destroyer key (value bits << 32 | position / pixel)
+      int c[2][REC_CAP];         // creator: cell position, then top-coface pixel
+      float cv[2][REC_CAP];      // creator value
+    } rec;
+  } u;
+  u16 vinv[MAXN];  // rank -> vertex id
+  u16 pinv[MAXN];  // rank -> pixel
+  int nlog[2], nrec[2];
   int overflow;
   float red_v[NTHR / 64];
   int red_i[NTHR / 64];
 };
 
-// Key of a union-find node. H1 nodes: pixels (key = value bits, pixel idx), exterior = +inf.
-__device__ __forceinline__ uint64_t pix_key(const Smem& s, int W, int node, int ext) {
-  return node == ext ? ~0ull : (((uint64_t)ord_bits(s.vals[node]) << 32) | (uint32_t)node);
-}
-// H0 nodes: vertices indexed by vertex id (vy*(W+1)+vx); key = (value bits, bitmap position).
-__device__ __forceinline__ uint64_t vert_key(const Map& m, int vid) {
-  int vx = vid % (m.W + 1), vy = vid / (m.W + 1);
-  int pos = 2 * vx + m.W2 * (2 * vy);
-  return ((uint64_t)ord_bits(cell_value(m, pos)) << 32) | (uint32_t)pos;
+// bitonic sort of NP2 64-bit keys, ascending; every thread owns NP2/2/NTHR compare-exchange pairs per
+// stage and issues all their loads before any store (one LDS latency per stage, not one per pair)
+__device__ void sort_keys(uint64_t* keys, int tid) {
+  constexpr int PP = NP2 / 2 / NTHR;
+  for (int k = 2; k <= NP2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t a[PP], b[PP];
+      int ia[PP];
+#pragma unroll
+      for (int t = 0; t < PP; ++t) {
+        const int q = tid + t * NTHR;
+        const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+        ia[t] = i;
+        a[t] = keys[i];
+        b[t] = keys[i | j];
+      }
+#pragma unroll
+      for (int t = 0; t < PP; ++t) {
+        const bool up = (ia[t] & k) == 0;
+        const bool sw = (a[t] > b[t]) == up;
+        const uint64_t lo = sw ? b[t] : a[t], hi = sw ? a[t] : b[t];
+        keys[ia[t]] = lo;
+        keys[ia[t] | j] = hi;
+      }
+      __syncthreads();
+    }
+  }
 }
 
-__device__ void h1_wave(Smem& s, const Map& m, int ne) {
+// vertex id <-> bitmap position
+__device__ __forceinline__ int vert_pos(const Map& m, int vid) { return 2 * (vid % (m.W + 1)) + m.W2 * 2 * (vid / (m.W + 1)); }
+__device__ __forceinline__ int pos_vert(const Map& m, int pos) { return (pos % m.W2) / 2 + (m.W + 1) * ((pos / m.W2) / 2); }
+
+// Elder-rule union-find over filtration RANKS (node id order == filtration order, so "younger" is an
+// integer comparison), 64 edges per chunk: lanes find their edge's roots against the chunk-start state in
+// parallel, then a wave-uniform loop resolves the 64 edges in order (readlane the two roots, min/max,
+// relabel every lane's roots, keep the merge in lane j). Merges are logged with ballot compaction
+// as (young rank << 13 | sorted edge index); filtering by positive persistence happens afterwards.
+// dim 0: vertices, edges increasing, younger = larger rank. dim 1: Alexander dual over pixels + exterior
+// (rank npix = +inf), edges decreasing, younger = smaller rank.
+template <int DIM>
+__device__ void uf_wave(Smem& s, const Map& m, int ne, int npix) {
   const int lane = threadIdx.x & 63;
-  const int ext = m.H * m.W;
+  const uint32_t* epos = (const uint32_t*)s.keys;
+  uint32_t* log = (uint32_t*)s.keys + NP2 + DIM * (m.H + 1) * (m.W + 1);  // H0 log <= nv-1, H1 log <= npix
+  u16* par = s.u.uf.par[DIM];
   int cnt = 0;
   for (int base = 0; base < ne; base += 64) {
-    const int idx = ne - 1 - (base + lane);  // decreasing filtration order
-    const bool valid = idx >= 0;
-    uint64_t ek = valid ? s.keys[idx] : 0;
-    int pos = (int)(uint32_t)ek;
-    int a = ext, c = ext;
+    const int idx = DIM == 0 ? base + lane : ne - 1 - (base + lane);
+    const bool valid = base + lane < ne;
+    int ru = 0, rv = 0;
     if (valid) {
-      int X = pos % m.W2, Y = pos / m.W2;
-      if (X & 1) {
-        int col = X >> 1;
-        a = (Y > 0) ? ((Y >> 1) - 1) * m.W + col : ext;
-        c = (Y < m.H2 - 1) ? (Y >> 1) * m.W + col : ext;
+      const int pos = (int)epos[idx];
+      const int X = pos % m.W2, Y = pos / m.W2;
+      if (DIM == 0) {
+        const int pu = (X & 1) ? pos - 1 : pos - m.W2, pv = (X & 1) ? pos + 1 : pos + m.W2;
+        ru = s.u.uf.vrank[pos_vert(m, pu)];
+        rv = s.u.uf.vrank[pos_vert(m, pv)];
       } else {
-        int row = Y >> 1;
-        a = (X > 0) ? row * m.W + (X >> 1) - 1 : ext;
-        c = (X < m.W2 - 1) ? row * m.W + (X >> 1) : ext;
-      }
-    }
-    int ra = valid ? uf_find(s.ppar, a) : ext;
-    int rc = valid ? uf_find(s.ppar, c) : ext;
-    uint64_t ka = pix_key(s, m.W, ra, ext), kc = pix_key(s, m.W, rc, ext);
-    int my_young = -1, my_old = -1;
-    const int nvalid = min(64, ne - base);
-    for (int j = 0; j < nvalid; ++j) {
-      int sa = __builtin_amdgcn_readlane(ra, j);
-      int sc = __builtin_amdgcn_readlane(rc, j);
-      if (sa == sc) continue;
-      uint64_t kka = readlane64(ka, j), kkc = readlane64(kc, j);
-      int young, old;
-      uint64_t kold;
-      if (kka < kkc) { young = sa; old = sc; kold = kkc; } else { young = sc; old = sa; kold = kka; }
-      if (ra == young) { ra = old; ka = kold; }
-      if (rc == young) { rc = old; kc = kold; }
-      if (lane == j) { my_young = young; my_old = old; }
-      // persistence > 0 ?  death value (young pixel) > edge value
-      uint64_t ekj = readlane64(ek, j);
-      float dv = s.vals[young];
-      float ev = unord_bits((uint32_t)(ekj >> 32));
-      if (dv > ev) {
-        if (lane == j) {
-          if (cnt < REC_CAP) {
-            s.rec_key[1][cnt] = ((uint64_t)ord_bits(dv) << 32) | (uint32_t)young;
-            s.rec_c[1][cnt] = top_coface(m, pos);
-          }
+        int a, c;
+        if (X & 1) {
+          const int col = X >> 1;
+          a = (Y > 0) ? ((Y >> 1) - 1) * m.W + col : -1;
+          c = (Y < m.H2 - 1) ? (Y >> 1) * m.W + col : -1;
+        } else {
+          const int row = Y >> 1;
+          a = (X > 0) ? row * m.W + (X >> 1) - 1 : -1;
+          c = (X < m.W2 - 1) ? row * m.W + (X >> 1) : -1;
         }
-        ++cnt;
+        ru = a < 0 ? npix : s.u.uf.prank[a];
+        rv = c < 0 ? npix : s.u.uf.prank[c];
       }
+      ru = uf_find(par, ru);
+      rv = uf_find(par, rv);
     }
-    if (my_young >= 0) s.ppar[my_young] = my_old;
+    int my_young = -1, my_old = 0;
+    // branch-free: an edge whose roots already agree relabels nothing (young == old) and is not recorded;
+    // the invalid tail lanes hold ru == rv == 0
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+      const int sa = __builtin_amdgcn_readlane(ru, j);
+      const int sc = __builtin_amdgcn_readlane(rv, j);
+      const int young = DIM == 0 ? max(sa, sc) : min(sa, sc);
+      const int old = DIM == 0 ? min(sa, sc) : max(sa, sc);
+      ru = ru == young ? old : ru;
+      rv = rv == young ? old : rv;
+      const bool rec = lane == j && sa != sc;
+      my_young = rec ? young : my_young;
+      my_old = rec ? old : my_old;
+    }
+    const bool merged = my_young >= 0;
+    if (merged) par[my_young] = (u16)my_old;
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(merged);
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    if (merged) log[cnt + below] = ((uint32_t)my_young << 13) | (uint32_t)idx;
+    cnt += __builtin_popcountll(mask);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
-  if (lane == 0) {
-    s.nrec[1] = min(cnt, REC_CAP);
-    if (cnt > REC_CAP) s.overflow |= 2;
-  }
-}
-
-__device__ void h0_wave(Smem& s, const Map& m, int ne) {
-  const int lane = threadIdx.x & 63;
-  int cnt = 0;
-  for (int base = 0; base < ne; base += 64) {
-    const int idx = base + lane;  // increasing filtration order
-    const bool valid = idx < ne;
-    uint64_t ek = valid ? s.keys[idx] : 0;
-    int pos = (int)(uint32_t)ek;
-    int u = 0, v = 0;
-    if (valid) {
-      int X = pos % m.W2;
-      int pu, pv;
-      if (X & 1) { pu = pos - 1; pv = pos + 1; } else { pu = pos - m.W2; pv = pos + m.W2; }
-      u = (pu % m.W2) / 2 + (m.W + 1) * ((pu / m.W2) / 2);
-      v = (pv % m.W2) / 2 + (m.W + 1) * ((pv / m.W2) / 2);
-    }
-    int ru = valid ? uf_find(s.vpar, u) : 0;
-    int rv = valid ? uf_find(s.vpar, v) : 0;
-    uint64_t ku = vert_key(m, ru), kv = vert_key(m, rv);
-    int my_young = -1, my_old = -1;
-    const int nvalid = min(64, ne - base);
-    for (int j = 0; j < nvalid; ++j) {
-      int su = __builtin_amdgcn_readlane(ru, j);
-      int sv = __builtin_amdgcn_readlane(rv, j);
-      if (su == sv) continue;
-      uint64_t kku = readlane64(ku, j), kkv = readlane64(kv, j);
-      int young, old;
-      uint64_t kold, kyoung;
-      if (kku > kkv) { young = su; old = sv; kold = kkv; kyoung = kku; }
-      else { young = sv; old = su; kold = kku; kyoung = kkv; }
-      if (ru == young) { ru = old; ku = kold; }
-      if (rv == young) { rv = old; kv = kold; }
-      if (lane == j) { my_young = young; my_old = old; }
-      uint64_t ekj = readlane64(ek, j);
-      float bv = unord_bits((uint32_t)(kyoung >> 32));
-      float ev = unord_bits((uint32_t)(ekj >> 32));
-      if (ev > bv) {
-        if (lane == j) {
-          if (cnt < REC_CAP) {
-            s.rec_key[0][cnt] = ekj;
-            s.rec_c[0][cnt] = top_coface(m, (int)(uint32_t)kyoung);
-          }
-        }
-        ++cnt;
-      }
-    }
-    if (my_young >= 0) s.vpar[my_young] = my_old;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  }
-  if (lane == 0) {
-    s.nrec[0] = min(cnt, REC_CAP);
-    if (cnt > REC_CAP) s.overflow |= 1;
-  }
+  if (lane == 0) s.nlog[DIM] = cnt;
 }
 
 __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restrict__ maps, int H, int W, int max_pairs,
@@ -242,16 +233,49 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
   __shared__ Smem s;
   const int tid = threadIdx.x;
   const int map = blockIdx.x;
-  const int npix = H * W;
+  const int npix = H * W, nv = (H + 1) * (W + 1);
   Map m{H, W, 2 * W + 1, 2 * H + 1, s.vals};
   const float* src = maps + (long long)map * npix;
+  PH_STAMP(0);
   for (int i = tid; i < npix; i += NTHR) s.vals[i] = src[i];
-  const int nh = (H + 1) * W, nvrt = H * (W + 1), ne = nh + nvrt;
-  int np2 = 1;
-  while (np2 < ne) np2 <<= 1;
-  if (tid == 0) { s.overflow = 0; }
+  if (tid == 0) {
+    s.overflow = 0;
+    s.nrec[0] = s.nrec[1] = 0;
+  }
   __syncthreads();
-  for (int i = tid; i < np2; i += NTHR) {
+  // 1. node filtration order: vertices (lower-star value, bitmap position) then pixels (value, index),
+  //    one sort; type bit 46 keeps the two lists apart
+  for (int i = tid; i < NP2; i += NTHR) {
+    uint64_t k = ~0ull;
+    if (i < nv) {
+      const int pos = vert_pos(m, i);
+      k = ((uint64_t)ord_bits(cell_value(m, pos)) << 14) | (uint32_t)pos;
+    } else if (i < nv + npix) {
+      const int px = i - nv;
+      k = (1ull << 46) | ((uint64_t)ord_bits(s.vals[px]) << 14) | (uint32_t)px;
+    }
+    s.keys[i] = k;
+  }
+  for (int i = tid; i <= npix; i += NTHR) s.u.uf.par[1][i] = (u16)i;
+  for (int i = tid; i < nv; i += NTHR) s.u.uf.par[0][i] = (u16)i;
+  __syncthreads();
+  PH_STAMP(1);
+  sort_keys(s.keys, tid);
+  for (int i = tid; i < nv + npix; i += NTHR) {
+    const int low = (int)(s.keys[i] & 0x3fff);
+    if (i < nv) {
+      const int vid = pos_vert(m, low);
+      s.vinv[i] = (u16)vid;
+      s.u.uf.vrank[vid] = (u16)i;
+    } else {
+      s.pinv[i - nv] = (u16)low;
+      s.u.uf.prank[low] = (u16)(i - nv);
+    }
+  }
+  __syncthreads();
+  // 2. edge (1-cell) order: (lower-star value, bitmap position) -> sorted positions epos
+  const int nh = (H + 1) * W, nvrt = H * (W + 1), ne = nh + nvrt;
+  for (int i = tid; i < NP2; i += NTHR) {
     uint64_t k = ~0ull;
     if (i < ne) {
       int X, Y;
@@ -262,32 +286,27 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     }
     s.keys[i] = k;
   }
-  for (int i = tid; i < (H + 1) * (W + 1); i += NTHR) s.vpar[i] = i;
-  for (int i = tid; i <= npix; i += NTHR) s.ppar[i] = i;
   __syncthreads();
-  // bitonic sort ascending
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < np2; i += NTHR) {
-        int l = i ^ j;
-        if (l > i) {
-          uint64_t a = s.keys[i], b = s.keys[l];
-          bool up = (i & k) == 0;
-          if ((a > b) == up) { s.keys[i] = b; s.keys[l] = a; }
-        }
-      }
-      __syncthreads();
-    }
+  sort_keys(s.keys, tid);
+  {
+    uint32_t ep[NP2 / NTHR];
+#pragma unroll
+    for (int t = 0; t < NP2 / NTHR; ++t) ep[t] = (uint32_t)s.keys[tid + t * NTHR];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NP2 / NTHR; ++t) ((uint32_t*)s.keys)[tid + t * NTHR] = ep[t];
   }
+  __syncthreads();
   const int wave = tid >> 6;
-  if (wave == 0) h1_wave(s, m, ne);
-  else if (wave == 1) h0_wave(s, m, ne);
+  PH_STAMP(2);
+  if (wave == 0) uf_wave<1>(s, m, ne, npix);
+  else if (wave == 1) uf_wave<0>(s, m, ne, npix);
+  if (wave == 0) PH_STAMP_W(3);
+  if (wave == 1) PH_STAMP_W(4);
   __syncthreads();
+  PH_STAMP(5);
 
-  // essential class root (oldest vertex) and argmax pixel (first maximum) by block reduction.
-  if (wave == 2 || wave == 3) {
-    // nothing: handled below by all threads
-  }
+  // essential H0 class (root of vertex 0's tree, oldest vertex) and argmax pixel (first maximum)
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   for (int i = tid; i < npix; i += NTHR) {
@@ -300,45 +319,95 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
   }
   if ((tid & 63) == 0) { s.red_v[wave] = bv; s.red_i[wave] = bi; }
-  __syncthreads();
+  int root_vid = 0;
+  if (tid == 0) root_vid = s.vinv[uf_find(s.u.uf.par[0], s.u.uf.vrank[0])];
+  __syncthreads();  // the union-find arrays are dead from here: their bytes hold the pair records
   if (tid == 0) {
     float v = s.red_v[0];
     int ii = s.red_i[0];
     for (int w = 1; w < NTHR / 64; ++w)
       if (s.red_v[w] > v || (s.red_v[w] == v && s.red_i[w] < ii)) { v = s.red_v[w]; ii = s.red_i[w]; }
-    int root = uf_find(s.vpar, 0);
-    int vx = root % (W + 1), vy = root / (W + 1);
-    essential[2 * map] = top_coface(m, 2 * vx + m.W2 * 2 * vy);
+    essential[2 * map] = top_coface(m, vert_pos(m, root_vid));
     essential[2 * map + 1] = ii;
+  }
+  // 3. keep the merges with positive persistence (death value > birth value) -> records
+  const uint32_t* epos = (const uint32_t*)s.keys;
+  for (int d = 0; d < 2; ++d) {
+    const uint32_t* log = (const uint32_t*)s.keys + NP2 + d * nv;
+    const int n = s.nlog[d];
+    for (int i = tid; i < n; i += NTHR) {
+      const uint32_t e = log[i];
+      const int young = (int)(e >> 13), pos = (int)epos[e & 0x1fff];
+      const float ev = cell_value(m, pos);
+      uint64_t key;
+      int cpos;
+      bool keep;
+      if (d == 0) {  // birth: the young vertex; death: the edge
+        const int vpos = vert_pos(m, s.vinv[young]);
+        keep = ev > cell_value(m, vpos);
+        key = ((uint64_t)ord_bits(ev) << 32) | (uint32_t)pos;
+        cpos = vpos;
+      } else {       // birth: the edge; death: the young pixel
+        const int px = s.pinv[young];
+        const float dv = s.vals[px];
+        keep = dv > ev;
+        key = ((uint64_t)ord_bits(dv) << 32) | (uint32_t)px;
+        cpos = pos;
+      }
+      if (keep) {
+        const int r = atomicAdd(&s.nrec[d], 1);
+        if (r < REC_CAP) {
+          s.u.rec.key[d][r] = key;
+          s.u.rec.c[d][r] = cpos;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // creator cells -> top-dimensional cofaces and their values
+  for (int d = 0; d < 2; ++d) {
+    const int n = min(s.nrec[d], REC_CAP);
+    for (int i = tid; i < n; i += NTHR) {
+      const int c = top_coface(m, s.u.rec.c[d][i]);
+      s.u.rec.c[d][i] = c;
+      s.u.rec.cv[d][i] = s.vals[c];
+    }
+  }
+  __syncthreads();
+  PH_STAMP(6);
+  if (tid == 0) {
+    if (s.nrec[0] > REC_CAP) s.overflow |= 1;
+    if (s.nrec[1] > REC_CAP) s.overflow |= 2;
     counts[3 * map + 0] = min(s.nrec[0], max_pairs);
     counts[3 * map + 1] = min(s.nrec[1], max_pairs);
     counts[3 * map + 2] = (s.overflow || s.nrec[0] > max_pairs || s.nrec[1] > max_pairs) ? 1 : 0;
   }
-  // rank pairs: (persistence desc, destroyer key asc); persistence in double like gudhi
+  // 4. rank pairs: (persistence desc, destroyer key asc) -- a total order, so the output does not depend on
+  //    the record order; persistence in double like gudhi
   for (int d = 0; d < 2; ++d) {
-    const int n = s.nrec[d];
+    const int n = min(s.nrec[d], REC_CAP);
     int* out = d == 0 ? pairs0 : pairs1;
     for (int i = tid; i < n; i += NTHR) {
-      uint64_t ki = s.rec_key[d][i];
-      int ci = s.rec_c[d][i];
-      double pi = (double)unord_bits((uint32_t)(ki >> 32)) - (double)s.vals[ci];
+      const uint64_t ki = s.u.rec.key[d][i];
+      const int ci = s.u.rec.c[d][i];
+      const double pi = (double)unord_bits((uint32_t)(ki >> 32)) - (double)s.u.rec.cv[d][i];
       int rank = 0;
       for (int j = 0; j < n; ++j) {
-        uint64_t kj = s.rec_key[d][j];
-        double pj = (double)unord_bits((uint32_t)(kj >> 32)) - (double)s.vals[s.rec_c[d][j]];
+        const uint64_t kj = s.u.rec.key[d][j];
+        const double pj = (double)unord_bits((uint32_t)(kj >> 32)) - (double)s.u.rec.cv[d][j];
         rank += (pj > pi) || (pj == pi && kj < ki);
       }
       if (rank < max_pairs) {
-        int dpix;
-        int pos = (int)(uint32_t)ki;
-        if (d == 1) dpix = pos;  // H1 records store the destroyer pixel index directly
-        else dpix = top_coface(m, pos);
+        const int pos = (int)(uint32_t)ki;
+        const int dpix = d == 1 ? pos : top_coface(m, pos);  // H1 records hold the destroyer pixel itself
         long long o = ((long long)map * max_pairs + rank) * 2;
         out[o] = ci;
         out[o + 1] = dpix;
       }
     }
   }
+  __syncthreads();
+  PH_STAMP(7);
 }
 
 }  // namespace
@@ -348,8 +417,9 @@ extern "C" int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, in
                                  void* stream) {
   OCTSAM_CHECK_ARG(maps && pairs0 && pairs1 && essential && counts, "octsam_cubical_ph: null pointer");
   OCTSAM_CHECK_ARG(nmaps >= 0 && H >= 1 && W >= 1 && max_pairs >= 1, "octsam_cubical_ph: bad sizes");
-  OCTSAM_CHECK_ARG(H * W <= MAX_PIX && H <= 64 && W <= 64, "octsam_cubical_ph: map %dx%d too large (<=64x64)", H, W);
-  OCTSAM_CHECK_ARG((H + 1) * W + H * (W + 1) <= MAX_EDGES_POW2, "octsam_cubical_ph: too many edges");
+  OCTSAM_CHECK_ARG(H * W <= MAX_PIX && (H + 1) * W + H * (W + 1) <= NP2 && (H + 1) * (W + 1) + H * W <= NP2 &&
+                       (2 * W + 1) * (2 * H + 1) <= 16384,
+                   "octsam_cubical_ph: map %dx%d too large (<= 63x63)", H, W);
   if (nmaps == 0) return 0;
   hipLaunchKernelGGL(cubical_ph_kernel, dim3(nmaps), dim3(NTHR), 0, (hipStream_t)stream, maps, H, W, max_pairs,
                      pairs0, pairs1, essential, counts);
