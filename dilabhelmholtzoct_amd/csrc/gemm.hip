@@ -70,18 +70,21 @@ __device__ __forceinline__ bf16x8 cvt8(const float4 a, const float4 b) {
   return r;
 }
 
-// Stage: each thread holds 4 chunks of 8 bf16 for the operand tile (128 rows x 64 k).
-template <int MODE>
+// Stage: each thread holds R/32 chunks of 8 bf16 for the operand tile (R rows x 64 k).
+template <int MODE, int R = 128>
 struct Loader {
-  bf16x8 v[4];
+  static constexpr int NC = R / 32;  // chunks per thread
+  static constexpr int RC = R / 8;   // 8-row chunks per k row (transposed modes)
+  bf16x8 v[NC];
 
   __device__ __forceinline__ void load(const GemmK& p, const void* base, const void* add, int period,
-                                       long long ld, int rows, int row0, int k0, int tid, int blk, int rep) {
+                                       long long ld, int rows, int row0, int k0, int tid, int blk, int rep,
+                                       int kcap) {
     if constexpr (MODE == 4) {
       const bf16* src = (const bf16*)base;
       const bf16* ad = (const bf16*)add;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
@@ -99,9 +102,9 @@ struct Loader {
       const bf16* src = (const bf16*)base;
       const bf16* ad = (const bf16*)add;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
-        int k = ci >> 4, rc = ci & 15;
+        int k = ci / RC, rc = ci % RC;
         int gr = row0 + rc * 8, gk = k0 + k;
         if (gr < rows && gk < p.K) {
           bf16x8 x = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
@@ -116,7 +119,7 @@ struct Loader {
     } else if constexpr (MODE == 0) {
       const bf16* src = (const bf16*)base;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
@@ -128,11 +131,11 @@ struct Loader {
     } else if constexpr (MODE == 1) {
       const bf16* src = (const bf16*)base;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
-        int k = ci >> 4, rc = ci & 15;
+        int k = ci / RC, rc = ci % RC;
         int gr = row0 + rc * 8, gk = k0 + k;
-        if (gr < rows && gk < p.K)
+        if (gr < rows && gk < kcap)
           v[i] = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
         else
           v[i] = (bf16x8)(bf16)0.0f;
@@ -140,7 +143,7 @@ struct Loader {
     } else if constexpr (MODE == 2) {
       const float* px = (const float*)base;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
@@ -159,7 +162,7 @@ struct Loader {
       const bf16* src = (const bf16*)base;
       const int C = p.conv_c;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
@@ -179,9 +182,9 @@ struct Loader {
   __device__ __forceinline__ void store(bf16* lds, int tid) {
     if constexpr (MODE == 1 || MODE == 5) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
-        int k = ci >> 4, rc = ci & 15;
+        int k = ci / RC, rc = ci % RC;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           int r = rc * 8 + e;
@@ -190,7 +193,7 @@ struct Loader {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         *(bf16x8*)(lds + lds_idx(r, c)) = v[i];
@@ -199,9 +202,11 @@ struct Loader {
   }
 };
 
-template <int AM, int BMODE>
+// T = 128 (block tile 128x128, wave 64x64) or 64 (block 64x64, wave 32x32: small problems, 4x the blocks)
+template <int AM, int BMODE, int T = 128>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+  constexpr int MB = T / 64;  // 32x32 MFMA blocks per wave and dimension
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (T + T) * BK];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
     bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
   }
   const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
-  const int row0 = tm * BM, col0 = tn * BN;
+  const int row0 = tm * T, col0 = tn * T;
   const int bz = blockIdx.y;
 
   const char* Ab = (const char*)p.A;
@@ -223,47 +228,49 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
   const void* Abase = (AM == 2) ? (const void*)(Ab + bz * p.sA * 4) : (const void*)(Ab + bz * p.sA * 2);
   const void* Bbase = (const void*)(Bb + bz * p.sB * 2);
 
-  Loader<AM> la;
-  Loader<BMODE> lb;
-  f32x16 acc[2][2];
+  Loader<AM, T> la;
+  Loader<BMODE, T> lb;
+  f32x16 acc[MB][MB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
+    for (int j = 0; j < MB; ++j) acc[i][j] = (f32x16)0.0f;
+  // split-K over k-major operands (k_total): rows past k_total (counted from batch 0) read as zero
+  const int kcap = p.k_total > 0 ? min(p.K, p.k_total - bz * p.K) : p.K;
 
   const int nk = (p.K + BK - 1) / BK;
-  la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, 0, tid, p.a_blk, p.a_rep);
-  lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, 0, tid, p.b_blk, p.b_rep);
+  la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, 0, tid, p.a_blk, p.a_rep, kcap);
+  lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, 0, tid, p.b_blk, p.b_rep, kcap);
   la.store(smem, tid);
-  lb.store(smem + BM * BK, tid);
+  lb.store(smem + T * BK, tid);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
-    bf16* sa = smem + (kt & 1) * (BM + BN) * BK;
-    bf16* sb = sa + BM * BK;
+    bf16* sa = smem + (kt & 1) * (T + T) * BK;
+    bf16* sb = sa + T * BK;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid, p.a_blk, p.a_rep);
-      lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, (kt + 1) * BK, tid, p.b_blk, p.b_rep);
+      la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid, p.a_blk, p.a_rep, kcap);
+      lb.load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, (kt + 1) * BK, tid, p.b_blk, p.b_rep, kcap);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const int ch = kk * 2 + (lane >> 5);
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[MB], bfr[MB];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sa + lds_idx(wm * 64 + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(sa + lds_idx(wm * (T / 2) + i * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = *(const bf16x8*)(sb + lds_idx(wn * 64 + j * 32 + (lane & 31), ch));
+      for (int j = 0; j < MB; ++j) bfr[j] = *(const bf16x8*)(sb + lds_idx(wn * (T / 2) + j * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MB; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < MB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      bf16* na = smem + ((kt + 1) & 1) * (BM + BN) * BK;
+      bf16* na = smem + ((kt + 1) & 1) * (T + T) * BK;
       la.store(na, tid);
-      lb.store(na + BM * BK, tid);
+      lb.store(na + T * BK, tid);
     }
     __syncthreads();
   }
@@ -273,15 +280,15 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
   const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
   char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = col0 + wn * 64 + j * 32 + (lane & 31);
+  for (int j = 0; j < MB; ++j) {
+    const int n = col0 + wn * (T / 2) + j * 32 + (lane & 31);
     if (n >= p.N) continue;
     const float bv = p.bias ? p.bias[n] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MB; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = row0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int m = row0 + wm * (T / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= p.M) continue;
         int om = m;
         if (p.row_map) {
@@ -309,10 +316,13 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
   }
 }
 
-template <int AM, int BMODE>
-int launch(const GemmK& k, int batch, hipStream_t s) {
+template <int AM, int BMODE, int T = 128>
+int launch(const GemmK& k0, int batch, hipStream_t s) {
+  GemmK k = k0;
+  k.tiles_m = (k.M + T - 1) / T;
+  k.tiles_n = (k.N + T - 1) / T;
   dim3 grid(k.tiles_m * k.tiles_n, batch);
-  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NTHR), 0, s, k);
+  hipLaunchKernelGGL((gemm_kernel<AM, BMODE, T>), grid, dim3(NTHR), 0, s, k);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
 }
@@ -1397,8 +1407,14 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 }  // namespace
 
 static int g_use_glds = 1;
+static int g_small = 1;
 static thread_local int t_last_path = 0;
-extern "C" void octsam_gemm_set_fast_path(int32_t enable) { g_use_glds = enable; }
+// enable: 0 = generic kernels only; 1 = default; 2..10 = fast-path variants (diagnostics); bit 8 (256)
+// disables the small-problem 64x64 path
+extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
+  g_small = (enable & 256) ? 0 : 1;
+  g_use_glds = enable & 255;
+}
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
 
 extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
@@ -1444,6 +1460,19 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   const bool fast_epi = (a->N & 1) == 0 && (a->ldc & 1) == 0 && ((uintptr_t)a->C & 7) == 0 &&
                         (!a->C_pre || ((uintptr_t)a->C_pre & 7) == 0) &&
                         (!a->R || ((a->ldr & 1) == 0 && ((uintptr_t)a->R & 7) == 0));
+  // Small problems (token-side decoder GEMMs: M ~ P*7 rows, split-K weight gradients): a 256-row tile
+  // leaves most CUs idle, so the register-staged kernel with 64x64 tiles takes them.
+  {
+    const long long t64 = (long long)((a->M + 63) / 64) * ((a->N + 63) / 64) * a->batch;
+    const long long t256 = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
+    if (am <= 1 && bm <= 1 && a->a_blk == 0 && a->b_blk == 0 && t256 < 96 && t64 <= 4096 && g_small) {
+      t_last_path = 3;
+      if (am == 0 && bm == 0) return launch<0, 0, 64>(k, a->batch, s);
+      if (am == 0 && bm == 1) return launch<0, 1, 64>(k, a->batch, s);
+      if (am == 1 && bm == 0) return launch<1, 0, 64>(k, a->batch, s);
+      return launch<1, 1, 64>(k, a->batch, s);
+    }
+  }
   // persistent LDS-DMA kernel: K-contiguous (mode 0) or k-major (mode 1, transposed-read) operands
   const bool ok_a = (a->lda & 7) == 0 && (am == 0 || (am == 1 && (a->M & 7) == 0 && a->M >= 8));
   const bool ok_b = (a->ldb & 7) == 0 && (bm == 0 || (bm == 1 && (a->N & 7) == 0 && a->N >= 8));
@@ -1484,7 +1513,7 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
     return launch_glds<256, 64, 2>(k, a, s);
   }
   t_last_path = 0;
-  OCTSAM_CHECK_ARG(a->k_total == 0, "octsam_gemm: k_total tail needs the LDS-DMA path (ld/M/N %% 8, enough tiles)");
+  OCTSAM_CHECK_ARG(a->k_total == 0 || (am == 1 && bm == 1), "octsam_gemm: k_total needs a_mode = b_mode = 1");
   if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);
   if (am == 0 && bm == 1) return launch<0, 1>(k, a->batch, s);
   if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);

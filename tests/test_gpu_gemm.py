@@ -144,7 +144,7 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     # 1: 8-phase kernel, one tile per workgroup (register epilogue; beta != 0 goes to the ring kernel), 10: persistent
     # 8-phase, 8: 8-phase with the LDS-staged epilogue, 5: persistent ring kernel, 0: generic
     for fast in (1, 10, 8, 5, 0):
-        lib.octsam_gemm_set_fast_path(fast)
+        lib.octsam_gemm_set_fast_path(fast | 256)  # 256: keep this shape off the small-problem path
         out = C0.clone()
         pout = None if pre is None else torch.zeros(Bt, M, N, device=cuda,
                                                     dtype=torch.float32 if pre == "f32" else torch.bfloat16)
@@ -186,9 +186,10 @@ def test_gemm8_register_epilogue_act(cuda, act, M, N, K):
     bias = torch.randn(N, generator=g).to(cuda)
     R = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    lib.octsam_gemm_set_fast_path(1)
+    lib.octsam_gemm_set_fast_path(1 | 256)
     kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, act=act, residual=R)
     assert lib.octsam_gemm_last_path() == 2
+    lib.octsam_gemm_set_fast_path(1)
     pre = A.float() @ W.float().t() + bias
     ref = {0: pre, 1: F.relu(pre), 2: F.gelu(pre)}[act] + R.float()
     assert _rel(out, ref) < 8e-3
@@ -211,7 +212,7 @@ def test_gemm_fast_path_kmajor(cuda, a_mode, b_mode, shape):
     R = torch.randn(Bt, M, N, generator=g).to(cuda, torch.bfloat16)
     ref = F.relu(torch.bmm(A.float(), W.float().transpose(1, 2)).to(cuda) + bias) + R.float()
     for fast in (1, 0):
-        lib.octsam_gemm_set_fast_path(fast)
+        lib.octsam_gemm_set_fast_path(fast | 256)
         out = torch.empty(Bt, M, N, device=cuda, dtype=torch.float32)
         kernels.gemm(Aop, Bop, M=M, N=N, K=K, out=out, a_mode=a_mode, b_mode=b_mode, batch=Bt, stride_a=M * K,
                      stride_b=N * K, stride_c=M * N, stride_r=M * N, bias=bias, act=1, residual=R)
@@ -234,3 +235,46 @@ def test_dw_ragged_splitk(cuda, Mtok, O, I):
     MaskDecoder._dw(MaskDecoder, dy, x, Mtok, out)
     ref = dy.float().t() @ x.float()
     assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("a_mode,b_mode", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("shape", [(1120, 256, 256, 1), (160, 32, 256, 1), (256, 256, 64, 18), (72, 200, 136, 3)])
+def test_gemm_small_path(cuda, a_mode, b_mode, shape):
+    """Small problems (token-side decoder GEMMs, split-K weight gradients) on the 64x64-tile kernel: every
+    operand mode, batches, bias/ReLU/fp32 residual epilogue, against torch fp32."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    M, N, K, Bt = shape
+    g = torch.Generator().manual_seed(M * 3 + N + K + a_mode * 5 + b_mode)
+    A = torch.randn(Bt, M, K, generator=g).to(torch.bfloat16)
+    W = torch.randn(Bt, N, K, generator=g).to(torch.bfloat16)
+    Aop = (A if a_mode == 0 else A.transpose(1, 2)).contiguous().to(cuda)
+    Bop = (W if b_mode == 0 else W.transpose(1, 2)).contiguous().to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(Bt, M, N, generator=g).to(cuda)
+    out = torch.empty(Bt, M, N, device=cuda, dtype=torch.float32)
+    kernels.gemm(Aop, Bop, M=M, N=N, K=K, out=out, a_mode=a_mode, b_mode=b_mode, batch=Bt, stride_a=M * K,
+                 stride_b=N * K, stride_c=M * N, stride_r=M * N, bias=bias, act=1, residual=R)
+    assert lib.octsam_gemm_last_path() == 3
+    ref = F.relu(torch.bmm(A.float(), W.float().transpose(1, 2)).to(cuda) + bias) + R
+    assert _rel(out, ref) < 1e-5
+
+
+def test_gemm_small_path_ktotal(cuda):
+    """Split-K with a ragged total (k_total): rows past k_total read as zero on the small-problem path."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    rows, O, I, ks = 1130, 256, 128, 64
+    splits = -(-rows // ks)
+    g = torch.Generator().manual_seed(11)
+    dy = torch.randn(splits * ks, O, generator=g)
+    x = torch.randn(splits * ks, I, generator=g)
+    dy[rows:] = float("nan")  # must never be read
+    x[rows:] = float("nan")
+    dyb, xb = dy.to(cuda, torch.bfloat16), x.to(cuda, torch.bfloat16)
+    part = torch.empty(splits, O, I, device=cuda)
+    kernels.gemm(dyb, xb, M=O, N=I, K=ks, out=part, a_mode=1, b_mode=1, lda=O, ldb=I, batch=splits,
+                 stride_a=ks * O, stride_b=ks * I, stride_c=O * I, k_total=rows)
+    assert lib.octsam_gemm_last_path() == 3
+    ref = dyb[:rows].float().t() @ xb[:rows].float()
+    assert _rel(part.sum(0), ref) < 1e-5
