@@ -27,6 +27,9 @@ import torch  # noqa: E402
 
 METRIC = "train imgs/sec (1024² OCT, vit-base, top-loss on) + val Dice; 1→8 GPUs"
 MI355X_BF16_DENSE_TFLOPS = 2500.0  # /opt/skills/guides/MI355X_MICROARCH.md (dense, no sparsity)
+# HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x2 for
+# gfx950's half-counted wide reads + WRITE_SIZE; scripts/gpu_round.sh -> scripts/pmc_traffic.py), same bench
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_gemm8.json")
 
 
 def log(msg):
@@ -67,6 +70,7 @@ class GemmEventTimer:
         self.active = False
         self.events = []
         self.flops = 0.0
+        self.bytes = 0.0
 
     def __enter__(self):
         orig = self.orig
@@ -84,6 +88,12 @@ class GemmEventTimer:
                 if lib.octsam_gemm_last_path() == 2:
                     self.events.append((s, e))
                     self.flops += 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
+                    # compulsory bytes: A, B read once, C written once (+ residual read), per launch
+                    bt = kw.get("batch", 1)
+                    osz = kw["out"].element_size()
+                    r = kw.get("residual")
+                    self.bytes += bt * (2.0 * (kw["M"] + kw["N"]) * kw["K"] + kw["M"] * kw["N"] * osz +
+                                        (kw["M"] * kw["N"] * r.element_size() if r is not None else 0))
                 return out
             return orig(A, B, **kw)
 
@@ -217,9 +227,14 @@ def main():
         ms, n, flops = timer.result()
         if n:
             achieved = flops / (ms * 1e-3) / 1e12
+            traffic = None
+            if os.path.exists(TRAFFIC_JSON):
+                traffic = round(json.load(open(TRAFFIC_JSON))["hbm_bytes_per_launch"])
             roof = {"bound": "mfma", "kernel": DOMINANT,
                     "achieved": round(achieved, 2), "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / MI355X_BF16_DENSE_TFLOPS, 4), "traffic": None,
+                    "frac": round(achieved / MI355X_BF16_DENSE_TFLOPS, 4), "traffic": traffic,
+                    "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic is not None else None,
+                    "compulsory_bytes_per_launch": round(timer.bytes / n),
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}
 

@@ -258,6 +258,21 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <int N>
+__device__ __forceinline__ void tie_wait(s16x4 (&v)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]) : "n"(N));
+}
+
+// ds_read_b64_tr_b16 as inline asm: the builtin carries no memory operand, so hipcc assumes it may read
+// the LDS-DMA ring and drains every in-flight global_load_lds (s_waitcnt vmcnt(0)) in front of it, which
+// serialises the K/V prefetch. The caller waits lgkmcnt itself before using the result.
+__device__ __forceinline__ s16x4 tr_read_asm(const char* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 // 32 table rows j0 .. j0+31 of P^T = R · Qs^T (times 8: undo the 1/8 folded into Qs), rows >= nrows zero.
 __device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows, const bf16x8 (&qf)[4],
                                             int lane) {
@@ -393,17 +408,28 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
       for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
     }
     // O^T += V^T · P^T: P^T k-slot j of lane half hh is key 16ks + 8(j>>2) + 4hh + (j&3)
+    s16x4 vtr[4][2][2];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int td = 0; td < 2; ++td) {
         const int r0 = 16 * ks + 4 * (g >> 1) + qq;
         const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
-        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
-        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+        vtr[ks][td][0] = tr_read_asm(sv + vsw(r0, ch) + 8 * (pp & 1));
+        vtr[ks][td][1] = tr_read_asm(sv + vsw(r0 + 8, ch) + 8 * (pp & 1));
+      }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      // LDS returns in order: the first 4(ks+1) of the 16 reads are done at lgkmcnt(12 - 4ks); the asm ties
+      // the four registers so no use of them is scheduled ahead of the wait
+      if (ks == 0) tie_wait<12>(vtr[ks]);
+      else if (ks == 1) tie_wait<8>(vtr[ks]);
+      else if (ks == 2) tie_wait<4>(vtr[ks]);
+      else tie_wait<0>(vtr[ks]);
+      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int td = 0; td < 2; ++td) {
+        const s16x4 lo = vtr[ks][td][0], hi = vtr[ks][td][1];
         typedef short s16x8 __attribute__((ext_vector_type(8)));
         const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);
@@ -556,6 +582,153 @@ __global__ __launch_bounds__(W_THR) void vit_attn_window_kernel(const bf16* __re
     }
 }
 
+// ------------------------------------------------------------------------------------ window, v2
+// Same mapping as vit_attn_window_kernel (7 waves x 32 queries, the window's 196 keys padded to 256 and
+// masked, rel_w / rel_h from MFMA tables), with 64 KiB of LDS instead of 124 so that two workgroups share a
+// CU: K keeps the swizzled row image; V stays row-major (LDS image of global2's tr-read swizzle) and is
+// read transposed with ds_read_b64_tr_b16; the per-wave rel-pos tables are staged one after the other
+// through a scratch that overlays the V image before V is written. Key blocks that hold only padding
+// (keys 224..255: the second half of the last 64-key tile) are skipped.
+namespace w2 {
+constexpr int NW = 7, THR = NW * 64, KEYS = 256;
+constexpr int K_BYTES = KEYS * 128, V_BYTES = KEYS * 128;
+constexpr int SMEM = K_BYTES + V_BYTES;  // 64 KiB
+static_assert(NW * 32 * 33 * 4 <= V_BYTES, "rel-pos scratch must fit in the V image");
+}  // namespace w2
+
+__global__ __launch_bounds__(w2::THR, 2) void vit_attn_window2_kernel(const bf16* __restrict__ qkv,
+                                                                      bf16* __restrict__ out,
+                                                                      const float* __restrict__ Rh,
+                                                                      const float* __restrict__ Rw, int heads) {
+  using namespace g2;
+  constexpr int S = 14, T = 196;
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  char* kimg = wsm;
+  char* vimg = wsm + w2::K_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int head = blockIdx.y, win = blockIdx.x;
+  const int D = heads * 64, ld = 3 * D;
+  const bf16* base = qkv + (long long)win * T * ld;
+
+  // K rows (swizzled [256][64] image; keys >= 196 zero)
+  for (int ci = tid; ci < w2::KEYS * 8; ci += w2::THR) {
+    const int key = ci >> 3, c = ci & 7;
+    bf16x8 kv = (bf16x8)(bf16)0.0f;
+    if (key < T) kv = *(const bf16x8*)(base + (long long)key * ld + D + head * 64 + c * 8);
+    *(bf16x8*)(kimg + 2 * ksw(key, c)) = kv;
+  }
+  const int q = wave * 32 + l32;
+  const bool qvalid = q < T;
+  const int qh = qvalid ? q / S : 0, qw = qvalid ? q % S : 0;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+    qf[s4] = qvalid ? scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s4 + 8 * h))
+                    : (bf16x8)(bf16)0.0f;
+  // rel_w then rel_h through this wave's scratch (inside the V image; LDS ops of one wave run in order)
+  float* scr = (float*)vimg + wave * (32 * 33);
+  float relw[S], relh[S];
+  relpos_table<1>(Rw, 2 * S - 1, qf, scr, lane);
+#pragma unroll
+  for (int i = 0; i < S; ++i) relw[i] = scr[(qw - i + S - 1) * 33 + l32];
+  relpos_table<1>(Rh, 2 * S - 1, qf, scr, lane);
+#pragma unroll
+  for (int i = 0; i < S; ++i) relh[i] = scr[(qh - i + S - 1) * 33 + l32];
+  __syncthreads();  // every wave is done with its scratch: the V image may be written
+  for (int ci = tid; ci < w2::KEYS * 8; ci += w2::THR) {
+    const int key = ci >> 3, c = ci & 7;
+    bf16x8 vv = (bf16x8)(bf16)0.0f;
+    if (key < T) vv = *(const bf16x8*)(base + (long long)key * ld + 2 * D + head * 64 + c * 8);
+    *(bf16x8*)(vimg + vsw(key, c)) = vv;
+  }
+  __syncthreads();
+
+  f32x16 acc_o[2];
+  acc_o[0] = (f32x16)0.0f;
+  acc_o[1] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+  for (int tile = 0; tile < w2::KEYS / 64; ++tile) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int nb = tile == 3 ? 1 : 2;  // 32-key blocks holding a real key (keys < 224)
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      sacc[t2] = (f32x16)0.0f;
+      if (t2 < nb) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          bf16x8 a = *(const bf16x8*)(kimg + 2 * ksw(tile * 64 + t2 * 32 + l32, 2 * s4 + h));
+          sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s4], sacc[t2], 0, 0, 0);
+        }
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k0 = tile * 64 + t2 * 32 + acc_row(r, 0);
+        const int k1 = k0 + 4;
+        float b0 = (k0 < T) ? relh[(k0 < T ? k0 : 0) / S] + relw[(k0 < T ? k0 : 0) % S] : -INFINITY;
+        float b1 = (k1 < T) ? relh[(k1 < T ? k1 : 0) / S] + relw[(k1 < T ? k1 : 0) % S] : -INFINITY;
+        float v = sacc[t2][r] + (h ? b1 : b0);
+        sacc[t2][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.0f;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __expf(sacc[t2][r] - m_new);
+        sacc[t2][r] = pv;
+        ls += pv;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
+    // O^T += V^T P^T over the tile's real 16-key steps (the last tile: keys 192..207 only)
+    const char* sv = vimg + tile * 64 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (tile == 3 && ks > 0) break;
+      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+      for (int td = 0; td < 2; ++td) {
+        const int r0 = 16 * ks + 4 * (g >> 1) + qq;
+        const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
+        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
+        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);
+      }
+    }
+  }
+  if (!qvalid) return;
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  bf16* orow = out + ((long long)win * T + q) * D + head * 64;
+#pragma unroll
+  for (int td = 0; td < 2; ++td)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * gg + e] * inv);
+      *(bf16x4*)(orow + td * 32 + 8 * gg + 4 * h) = o;
+    }
+}
+
 }  // namespace
 
 static int g_attn_v2 = 1;
@@ -581,6 +754,16 @@ extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel
     dim3 grid(4096 / (G_NW * 32), heads, nseq);
     hipLaunchKernelGGL(vit_attn_global_kernel, grid, dim3(G_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
                        rel_pos_w, heads);
+  } else if (side == 14 && g_attn_v2) {
+    static bool wattr = false;
+    if (!wattr) {
+      (void)hipFuncSetAttribute((const void*)vit_attn_window2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                w2::SMEM);
+      wattr = true;
+    }
+    dim3 grid(nseq, heads, 1);
+    hipLaunchKernelGGL(vit_attn_window2_kernel, grid, dim3(w2::THR), w2::SMEM, s, (const bf16*)qkv, (bf16*)out,
+                       rel_pos_h, rel_pos_w, heads);
   } else if (side == 14) {
     dim3 grid(nseq, heads, 1);
     hipLaunchKernelGGL(vit_attn_window_kernel, grid, dim3(W_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
