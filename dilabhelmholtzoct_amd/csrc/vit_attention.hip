@@ -754,7 +754,7 @@ extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel
     dim3 grid(4096 / (G_NW * 32), heads, nseq);
     hipLaunchKernelGGL(vit_attn_global_kernel, grid, dim3(G_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
                        rel_pos_w, heads);
-  } else if (side == 14 && g_attn_v2) {
+  } else if (side == 14 && g_attn_v2 == 2) {  // (64 KiB variant; VGPR-bound to one workgroup per CU like v1)
     static bool wattr = false;
     if (!wattr) {
       (void)hipFuncSetAttribute((const void*)vit_attn_window2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
