@@ -459,7 +459,7 @@ class MaskDecoder(nn.Module):
             io_b = torch.empty(RL, CI, device=dev, dtype=b16)
             K.i2t_fwd(KQV[:, CI:], 3 * CI, kv_rep, Kt, Vt, P, T, L, io_b, CI)
             ls.i2t_o_b = io_b
-            s4 = torch.empty(RL, C, device=dev, dtype=f32)
+            s4 = torch.empty(RL, C, device=dev, dtype=b16)  # pre-LN4 keys stream: bf16 like keys_b (LN stats fp32)
             if li == 0:
                 self._lin(io_b, i2t + "out_proj.weight", i2t + "out_proj.bias", s4, RL, residual=imgd, r_remap=(L, N))
             else:
