@@ -10,7 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-    from dilabhelmholtzoct_amd import kernels
+    from dilabhelmholtzoct_amd import _lib, kernels
+    fast = int(os.environ.get("FAST", "1"))
+    _lib.load().octsam_gemm_set_fast_path(fast)
     M, N, K = (int(x) for x in sys.argv[1:4])
     act = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     f32 = int(sys.argv[5]) if len(sys.argv) > 5 else 0
@@ -30,7 +32,9 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / reps
-    print(f"M={M} N={N} K={K}: {us:.1f} us/launch, {2 * M * N * K / us / 1e6:.0f} TFLOP/s")
+    byts = 2 * (M + N) * K + M * N * out.element_size() * (2 if res else 1)
+    print(f"fast={fast} path={_lib.load().octsam_gemm_last_path()} M={M} N={N} K={K} act={act} f32={f32} res={res}: "
+          f"{us:.1f} us/launch, {2 * M * N * K / us / 1e6:.0f} TFLOP/s, {byts / us / 1e3:.0f} GB/s")
 
 
 if __name__ == "__main__":
