@@ -258,6 +258,12 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+__device__ __forceinline__ float max3_asm(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 template <int N>
 __device__ __forceinline__ void tie_wait(s16x4 (&v)[2][2]) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]) : "n"(N));
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
   const bf16* base = qkv + (long long)seq * T * ld;
   const int q = blockIdx.x * (NW * 32) + wave * 32 + l32;
   const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // static priority: the SIMD's two waves drift apart
 
   bf16x8 qf[4];
 #pragma unroll
@@ -333,11 +340,12 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
     for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * SCR_LD + l32] = t[r];
   }
   __syncthreads();
-  float relw[2][16];
+  // rel_w in natural units, as the initial accumulator of the S^T chain (free: the MFMA's C operand)
+  f32x16 relw[2];
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * SCR_LD + l32] * L2E;
+    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * SCR_LD + l32];
   __syncthreads();
   // rel_h table [kh][q]: row j = qh - kh + 63 -> block rows i = j - qh = 63 - kh
   float* relh = (float*)gsm + wave * (64 * 32);
@@ -369,36 +377,37 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
     if (tile + 2 < NT) load_tile(kbase, vbase, ld, tile + 2, ring + ((tile + 2) % NBUF) * TILE_BYTES, wave, lane);
     const char* sk = ring + (tile % NBUF) * TILE_BYTES;
     const char* sv = sk + 8192;
+    // S^T + rel_w (natural units): the chain starts from the rel_w registers
     f32x16 sacc[2];
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
-      sacc[t2] = (f32x16)0.0f;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const bf16x8 a = *(const bf16x8*)(sk + ksw_b(t2 * 32 + l32, 2 * s + h));
-        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
+        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], s == 0 ? relw[t2] : sacc[t2], 0, 0, 0);
       }
     }
+    // tile = key image row kh: rel_h is one constant per lane (log2 units), so max and exponent take it
+    // once per tile: p = exp2(L2E * s + (rh - m)), one FMA + one exp per score
     const float rh = relh[tile * 32 + l32];
-    float mx = -INFINITY;
+    // row max with v_max3 on the raw MFMA results (fmaxf would add a canonicalising v_max per value)
+    float mx = max3_asm(sacc[0][0], sacc[0][1], sacc[0][2]);
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
+    for (int r = 3; r < 15; r += 2) mx = max3_asm(mx, sacc[0][r], sacc[0][r + 1]);
+    mx = max3_asm(mx, sacc[0][15], sacc[1][0]);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v = fmaf(sacc[t2][r], L2E, relw[t2][r] + rh);
-        sacc[t2][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
+    for (int r = 1; r < 15; r += 2) mx = max3_asm(mx, sacc[1][r], sacc[1][r + 1]);
+    mx = max3_asm(mx, sacc[1][15], __shfl_xor(max3_asm(mx, sacc[1][15], sacc[1][15]), 32, 64));
+    const float m_new = fmaxf(m_run, fmaf(mx, L2E, rh));
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
+    const float c = rh - m_new;
     float ls = 0.0f;
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(sacc[t2][r] - m_new);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], L2E, c));
         sacc[t2][r] = pv;
         ls += pv;
       }
