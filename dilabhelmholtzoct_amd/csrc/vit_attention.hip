@@ -258,26 +258,7 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ float max3_asm(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
 
-template <int N>
-__device__ __forceinline__ void tie_wait(s16x4 (&v)[2][2]) {
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]) : "n"(N));
-}
-
-// ds_read_b64_tr_b16 as inline asm: the builtin carries no memory operand, so hipcc assumes it may read
-// the LDS-DMA ring and drains every in-flight global_load_lds (s_waitcnt vmcnt(0)) in front of it, which
-// serialises the K/V prefetch. The caller waits lgkmcnt itself before using the result.
-__device__ __forceinline__ s16x4 tr_read_asm(const char* p) {
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
 
 // 32 table rows j0 .. j0+31 of P^T = R · Qs^T (times 8: undo the 1/8 folded into Qs), rows >= nrows zero.
 __device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows, const bf16x8 (&qf)[4],
@@ -390,14 +371,14 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
     // tile = key image row kh: rel_h is one constant per lane (log2 units), so max and exponent take it
     // once per tile: p = exp2(L2E * s + (rh - m)), one FMA + one exp per score
     const float rh = relh[tile * 32 + l32];
-    // row max with v_max3 on the raw MFMA results (fmaxf would add a canonicalising v_max per value)
-    float mx = max3_asm(sacc[0][0], sacc[0][1], sacc[0][2]);
+    // (no inline-asm v_max3 here: hipcc's hazard recognizer does not see an asm statement read the MFMA
+    // result registers, and an early read made the row max -- and the rounding -- nondeterministic)
+    float mx = -INFINITY;
 #pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = max3_asm(mx, sacc[0][r], sacc[0][r + 1]);
-    mx = max3_asm(mx, sacc[0][15], sacc[1][0]);
+    for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-    for (int r = 1; r < 15; r += 2) mx = max3_asm(mx, sacc[1][r], sacc[1][r + 1]);
-    mx = max3_asm(mx, sacc[1][15], __shfl_xor(max3_asm(mx, sacc[1][15], sacc[1][15]), 32, 64));
+      for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sacc[t2][r], sacc[t2][r + 1]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, fmaf(mx, L2E, rh));
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
@@ -417,28 +398,17 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
       for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
     }
     // O^T += V^T · P^T: P^T k-slot j of lane half hh is key 16ks + 8(j>>2) + 4hh + (j&3)
-    s16x4 vtr[4][2][2];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
 #pragma unroll
       for (int td = 0; td < 2; ++td) {
         const int r0 = 16 * ks + 4 * (g >> 1) + qq;
         const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
-        vtr[ks][td][0] = tr_read_asm(sv + vsw(r0, ch) + 8 * (pp & 1));
-        vtr[ks][td][1] = tr_read_asm(sv + vsw(r0 + 8, ch) + 8 * (pp & 1));
-      }
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      // LDS returns in order: the first 4(ks+1) of the 16 reads are done at lgkmcnt(12 - 4ks); the asm ties
-      // the four registers so no use of them is scheduled ahead of the wait
-      if (ks == 0) tie_wait<12>(vtr[ks]);
-      else if (ks == 1) tie_wait<8>(vtr[ks]);
-      else if (ks == 2) tie_wait<4>(vtr[ks]);
-      else tie_wait<0>(vtr[ks]);
-      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
-#pragma unroll
-      for (int td = 0; td < 2; ++td) {
-        const s16x4 lo = vtr[ks][td][0], hi = vtr[ks][td][1];
+        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
+        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
         typedef short s16x8 __attribute__((ext_vector_type(8)));
         const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);

@@ -254,6 +254,20 @@ class MaskDecoder(nn.Module):
                a_mode=a_mode, A2=A2, a2_rows=a2_rows, lda=lda, ldc=ldc, pre_out=pre_out)
         return out
 
+    def _proj_pe(self, src_b, wnames, bnames, n_pe, out, M):
+        """out = src @ W^T + b + [pe @ W[:n_pe]^T | 0] for the grouped weights W (rows [k | q' | v]): the
+        keys + key-PE projections and the plain value projection of the same image-side input in ONE GEMM
+        over the M (= P*4096) rows; the PE enters as a row-periodic residual P[m % 4096] (P's first n_pe
+        columns = pe W^T + b, the rest = b), so the big product runs on the K-contiguous fast path."""
+        w = self._group(self.flat_b16, wnames, C)
+        b = self._group(self.flat, bnames, 0)
+        N = w.shape[0]
+        P = torch.empty(L_IMG, N, device=out.device, dtype=torch.bfloat16)
+        K.gemm(self._pe_b, w[:n_pe], M=L_IMG, N=n_pe, K=C, out=P, bias=b[:n_pe], ldc=N)
+        P[:, n_pe:].copy_(b[n_pe:].to(torch.bfloat16).expand(L_IMG, N - n_pe))
+        K.gemm(src_b, w, M=M, N=N, K=C, out=out, residual=P, ldr=N, r_remap=(L_IMG, max(1, M // L_IMG)), ldc=N)
+        return out
+
     @staticmethod
     def _pick_split(Mtok, O, I):
         """Split-K (splits, rows per split) for a weight gradient with Mtok reduction rows: enough (O x I tiles)
@@ -304,6 +318,17 @@ class MaskDecoder(nn.Module):
         K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, batch=split,
                stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I, k_total=M if Ks * split != M else 0)
         K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
+        return out
+
+    def _dw_pe(self, dy, x, M, out, n_pe, pe_b):
+        """Weight gradient of _proj_pe: out[o, i] = sum_m dy[m, o] x[m, i] for every grouped row o (one
+        k-major GEMM over the M rows), plus sum_p S[p, o] pe[p, i] for the first n_pe rows, S[p] = sum_j
+        dy[j*4096 + p] (the PE term)."""
+        O = out.shape[0]
+        self._dw(dy, x, M, out, ldy=O)
+        S = torch.empty(L_IMG, n_pe, device=out.device, dtype=torch.bfloat16)
+        K.group_sum(dy, S, ld_in=O, cols=n_pe, groups=1, nper=M // L_IMG, rows_per=L_IMG)
+        self._dw(S, pe_b, L_IMG, out[:n_pe], ldy=n_pe, accumulate=True)
         return out
 
     @staticmethod
@@ -393,6 +418,7 @@ class MaskDecoder(nn.Module):
         s.imgd, s.imgd_b = imgd, imgd_b
         pe_b = self._bf(pe)
         s.pe_b = pe_b
+        self._pe_b = pe_b
         s.layers = []
         queries, queries_b = None, None
         keys_b = None
@@ -428,10 +454,8 @@ class MaskDecoder(nn.Module):
             else:
                 src_b, M_kv, kv_rep = keys_b, RL, 1
             KQV = torch.empty(M_kv, 3 * CI, device=dev, dtype=b16)  # [K | Q' | V]
-            self._lin(src_b, None, None, KQV, M_kv, a_mode=4, A2=pe_b, a2_rows=L, ldc=3 * CI,
-                      wgroup=[t2i + "k_proj.weight", i2t + "q_proj.weight"],
-                      bgroup=[t2i + "k_proj.bias", i2t + "q_proj.bias"])
-            self._lin(src_b, t2i + "v_proj.weight", t2i + "v_proj.bias", KQV[:, 2 * CI:], M_kv, ldc=3 * CI)
+            self._proj_pe(src_b, [t2i + "k_proj.weight", i2t + "q_proj.weight", t2i + "v_proj.weight"],
+                          [t2i + "k_proj.bias", i2t + "q_proj.bias", t2i + "v_proj.bias"], 2 * CI, KQV, M_kv)
             ls.KQV, ls.kv_src_b, ls.kv_rep = KQV, src_b, kv_rep
             to_b = torch.empty(R, CI, device=dev, dtype=b16)
             lse = torch.empty(P, 8, T, device=dev, dtype=f32)
@@ -472,8 +496,8 @@ class MaskDecoder(nn.Module):
         s.f_qin_b = self._add_b16(queries, tok0)
         s.f_Q = self._lin(s.f_qin_b, f + "q_proj.weight", f + "q_proj.bias", torch.empty(R, CI, device=dev, dtype=f32), R)
         KV = torch.empty(RL, 2 * CI, device=dev, dtype=b16)
-        self._lin(keys_b, f + "k_proj.weight", f + "k_proj.bias", KV, RL, a_mode=4, A2=pe_b, a2_rows=L, ldc=2 * CI)
-        self._lin(keys_b, f + "v_proj.weight", f + "v_proj.bias", KV[:, CI:], RL, ldc=2 * CI)
+        self._proj_pe(keys_b, [f + "k_proj.weight", f + "v_proj.weight"], [f + "k_proj.bias", f + "v_proj.bias"], CI,
+                      KV, RL)
         s.f_KV = KV
         s.f_o_b = torch.empty(R, CI, device=dev, dtype=b16)
         s.f_lse = torch.empty(P, 8, T, device=dev, dtype=f32)
@@ -595,8 +619,8 @@ class MaskDecoder(nn.Module):
         # d keys2 += [dK | dV] @ [Wk; Wv]
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
         self._dx(dKV, wkv, RL, dkeys, beta=1.0)
-        self._dw(dKV, s.keys2_b, RL, self.G(f + "k_proj.weight"), ldy=2 * CI, x_add=s.pe_b, x_add_rows=L)
-        self._dw(dKV[:, CI:], s.keys2_b, RL, self.G(f + "v_proj.weight"), ldy=2 * CI)
+        self._dw_pe(dKV, s.keys2_b, RL, self._group(self.flat_grad, [f + "k_proj.weight", f + "v_proj.weight"], C),
+                    CI, s.pe_b)
         K.colsum(dKV, RL, 2 * CI, self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
         # ---- two-way blocks in reverse
         for li in reversed(range(cfg.num_hidden_layers)):
@@ -673,9 +697,8 @@ class MaskDecoder(nn.Module):
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
                 self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)
-                self._dw(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq, C), ldy=3 * CI, x_add=s.pe_b,
-                         x_add_rows=L)
-                self._dw(dKQV[:, 2 * CI:], ls.kv_src_b, RL, self.G(t2i + "v_proj.weight"), ldy=3 * CI)
+                self._dw_pe(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq + [t2i + "v_proj.weight"], C),
+                            2 * CI, s.pe_b)
                 K.colsum(dKQV, RL, 3 * CI, self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",
                                                                         t2i + "v_proj.bias"], 0))
                 dkeys = dkeys_in

@@ -114,3 +114,22 @@ def test_vit_attention(cuda, side, nseq, heads):
     ref = _ref_attention(qkv, Rh_b, Rw_b, nseq, side, heads)
     err = (out.float() - ref).abs().max().item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("side,nseq", [(14, 64), (64, 8)])
+def test_vit_attention_deterministic(cuda, side, nseq):
+    """Windowed (side 14) and global (side 64) attention at the encoder's shapes: repeated launches give
+    identical bits (graph replay must reproduce eager steps exactly; an early read of an MFMA result
+    register once made the global kernel's row max, and so its rounding, vary run to run)."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(side + nseq)
+    T = side * side
+    qkv = (0.5 * torch.randn(nseq * T, 3 * 768, generator=g)).to(cuda, torch.bfloat16)
+    Rh = (0.1 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
+    Rw = (0.1 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
+    outs = []
+    for _ in range(3):
+        o = torch.empty(nseq * T, 768, device=cuda, dtype=torch.bfloat16)
+        kernels.vit_attention(qkv, o, Rh, Rw, nseq=nseq, side=side, heads=12)
+        outs.append(o)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
