@@ -84,6 +84,10 @@ _SIGNATURES = {
     "octsam_mask_dot_fwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "octsam_mask_dot_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                       c_void_p, c_void_p]),
+    "octsam_upmask_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "octsam_upmask_bwd_workspace": (c_int64, [c_int32, c_int32]),
+    "octsam_upmask_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_postproc_fwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                       c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "octsam_dice_reduce": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),

@@ -1,0 +1,449 @@
+// Fused tail of SamMaskDecoder's upscaling + mask head (hf:modeling_sam.py:519-542):
+//   up2 = GELU(ConvT2(up1))  (ConvTranspose2d 64 -> 32, k2 s2, as a [rows, 64] x [64, 128] product)
+//   masks[p, t] = hyper[p, t] . up2                                    (mask = hyper_in @ upscaled)
+// forward and backward in one kernel each, so the 32-channel 256x256 upscaled embedding (and its
+// pre-activation and gradient) never touches HBM: the forward reads up1 and writes the masks; the
+// backward reads up1 and d masks, recomputes the ConvT2 product, and writes d up1 plus fixed-order
+// partials of d W2, d b2 and d hyper.
+//
+// Layout: up1 bf16 [P * 16384, 64] in the blocked order of the ConvT GEMMs (mask_head.hip): row =
+// (p, y1, x1, dy1, dx1), up2 column n = (dy2, dx2, c) -> pixel y = 4 y1 + 2 dy1 + dy2, x = 4 x1 + 2 dx1 + dx2.
+// A tile = 128 consecutive rows = (p, y1, half h of the x1 range), i.e. the mask block rows 4 y1 .. 4 y1 + 3,
+// columns 128 h .. 128 h + 127. Wave w owns tile rows 32 w .. 32 w + 31 (two 16-row MFMA blocks).
+// The product runs operand-swapped (A = W2 [n][k], B = up1 rows) so each lane holds one row (lane & 15)
+// and 4 consecutive n per 16-column block: the channel contraction with hyper is per lane + two xor
+// shuffles, and in the backward the same registers (bf16) are directly the B operand of d up1 = dpre W2^T
+// (the 8 k-slots of a lane are a permutation of n, matched in the W2^T fragments). d W2 = up1^T dpre
+// contracts over rows, so dpre and up1 are staged in LDS and read transposed (ds_read_b64_tr_b16).
+// Persistent workgroups (fixed grid, static tile stride) -> deterministic partial sums.
+#include "common.h"
+#include "../../include/octsam.h"
+
+namespace {
+namespace um {
+constexpr int ROWS = 128;               // up1 rows per tile
+constexpr int TILES_PER_P = 16384 / ROWS;
+constexpr int NWG = 512;                // persistent grid (2 workgroups per CU)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// A operand of the swapped product: lane (g, c), element j = W[n = 16 nb + c][k = 32 ks + 8 g + j] = w2[k][n]
+__device__ __forceinline__ void load_wfrag(const bf16* __restrict__ w2, bf16x8 (&wf)[8][2], int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wf[nb][ks][j] = w2[(32 * ks + 8 * g + j) * 128 + 16 * nb + c];
+}
+// B operand: lane (g, c) = up1 row (row0 + 16 rb + c), k = 32 ks + 8 g .. + 7 (one 16-B load)
+__device__ __forceinline__ void load_ufrag(const bf16* __restrict__ up1, long long row0, bf16x8 (&uf)[2][2],
+                                           int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) uf[rb][ks] = *(const bf16x8*)(up1 + (row0 + 16 * rb + c) * 64 + 32 * ks + 8 * g);
+}
+// pre^T block: acc[nb][i] = b2[n] + sum_k up1[row][k] W2[k][n], row = lane & 15 of block rb, n = 16 nb + 4 g + i
+__device__ __forceinline__ void convt2(const bf16x8 (&wf)[8][2], const bf16x8 (&ub)[2], const f32x4 (&binit)[8],
+                                       f32x4 (&acc)[8]) {
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) {
+    acc[nb] = mfma32(wf[nb][0], ub[0], binit[nb]);
+    acc[nb] = mfma32(wf[nb][1], ub[1], acc[nb]);
+  }
+}
+// (row within tile rr, sub-pixel s = 2 dy2 + dx2) -> offset in the tile's [4][128] mask block
+__device__ __forceinline__ int pix_local(int rr, int s) {
+  const int x1l = rr >> 2, dy1 = (rr >> 1) & 1, dx1 = rr & 1;
+  return (2 * dy1 + (s >> 1)) * 128 + 4 * x1l + 2 * dx1 + (s & 1);
+}
+// GELU (erf form) and its derivative from one shared erf / exp evaluation (A&S 7.1.26, |err| <= 1.5e-7)
+__device__ __forceinline__ void gelu_both(float x, float& y, float& dy) {
+  const float u = x * 0.70710678118654752f, au = fabsf(u);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, au, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-au * au);  // = exp(-x^2 / 2)
+  const float phi2 = 1.0f + copysignf(1.0f - p * t * e, u);
+  y = 0.5f * x * phi2;
+  dy = fmaf(x * 0.3989422804014327f, e, 0.5f * phi2);
+}
+}  // namespace um
+
+// grid: min(NWG, tiles) persistent workgroups of 256 threads; masks fp32 [P, NS, 256, 256]
+template <int NS>
+__global__ __launch_bounds__(256, 2) void upmask_fwd_kernel(const bf16* __restrict__ up1, const bf16* __restrict__ w2,
+                                                            const float* __restrict__ b2,
+                                                            const float* __restrict__ hyper, int ntiles,
+                                                            float* __restrict__ masks) {
+  using namespace um;
+  __shared__ __attribute__((aligned(16))) float smask[2][NS * 512];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  bf16x8 wf[8][2];
+  load_wfrag(w2, wf, lane);
+  f32x4 binit[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) binit[nb][i] = b2[(16 * nb + 4 * g + i) & 31];
+  bf16x8 nxt[2][2];
+  int T = blockIdx.x;
+  if (T < ntiles) load_ufrag(up1, (long long)T * ROWS + 32 * w, nxt, lane);
+  for (int it = 0; T < ntiles; T += gridDim.x, ++it) {
+    bf16x8 uf[2][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) uf[rb][0] = nxt[rb][0], uf[rb][1] = nxt[rb][1];
+    if (T + (int)gridDim.x < ntiles) load_ufrag(up1, (long long)(T + gridDim.x) * ROWS + 32 * w, nxt, lane);
+    const int p = T / TILES_PER_P, y1 = (T >> 1) & 63, h = T & 1;
+    f32x4 hy[NS][2];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) hy[t][hh] = *(const f32x4*)(hyper + (p * NS + t) * 32 + 16 * hh + 4 * g);
+    float* sm = smask[it & 1];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      f32x4 acc[8];
+      convt2(wf, uf[rb], binit, acc);
+      float m[NS][4];
+#pragma unroll
+      for (int t = 0; t < NS; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) m[t][s] = 0.0f;
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float u = gelu_fast(acc[nb][i]);
+#pragma unroll
+          for (int t = 0; t < NS; ++t) m[t][nb >> 1] = fmaf(hy[t][nb & 1][i], u, m[t][nb >> 1]);
+        }
+      // reduce-scatter over the 4 lane groups: group g ends with the full sum of sub-pixel s = g
+      const int rr = 32 * w + 16 * rb + c;
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        const bool hi2 = g & 2, hi1 = g & 1;
+        float a0 = hi2 ? m[t][2] : m[t][0], a1 = hi2 ? m[t][3] : m[t][1];
+        const float s0 = hi2 ? m[t][0] : m[t][2], s1 = hi2 ? m[t][1] : m[t][3];
+        a0 += __shfl_xor(s0, 32, 64);
+        a1 += __shfl_xor(s1, 32, 64);
+        float k = hi1 ? a1 : a0;
+        k += __shfl_xor(hi1 ? a0 : a1, 16, 64);
+        sm[t * 512 + pix_local(rr, g)] = k;
+      }
+    }
+    __syncthreads();  // (double-buffered staging: the buffer written next was last read before this barrier)
+    for (int e = tid; e < NS * 128; e += 256) {
+      const int t = e >> 7, yl = (e >> 5) & 3, x4 = (e & 31) * 4;
+      *(float4*)(masks + ((long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 128 * h + x4)) =
+          *(const float4*)(sm + t * 512 + yl * 128 + x4);
+    }
+  }
+}
+
+// Backward tiles are 64 rows = (p, y1, quarter q of the x1 range): mask block rows 4 y1 .. 4 y1 + 3, columns
+// 64 q .. 64 q + 63; wave w owns tile rows 16 w .. 16 w + 15 (one MFMA block) -- half the forward's tile,
+// for registers: the ConvT2 fragments (64 VGPRs) stay resident next to the d W2 accumulators.
+namespace um {
+constexpr int BROWS = 64;
+constexpr int BTILES_PER_P = 16384 / BROWS;
+constexpr int S_UP = 0;                       // up1 tile [64][64] bf16, 16-B chunk ^ (row & 7)
+constexpr int S_DP = S_UP + BROWS * 128;      // dpre tile [64][128] bf16, 16-B chunk ^ (row & 15)
+constexpr int S_W2T = S_DP + BROWS * 256;     // d up1 A-operand fragments [16][64 lanes] x 16 B
+constexpr int S_BIAS = S_W2T + 16 * 64 * 16;  // b2 per n [128] fp32
+constexpr int S_W2 = S_BIAS + 128 * 4;        // ConvT2 A-operand fragments [16][64 lanes] x 16 B
+constexpr int S_DM = S_W2 + 16 * 64 * 16;     // d masks of the tile [NS][4][64] fp32
+__device__ __forceinline__ int up_off(int r, int ch) { return S_UP + r * 128 + 16 * (ch ^ (r & 7)); }
+__device__ __forceinline__ int dp_off(int r, int ch) { return S_DP + r * 256 + 16 * (ch ^ (r & 15)); }
+__device__ __forceinline__ int bpix_local(int rr, int s) {
+  const int x1l = rr >> 2, dy1 = (rr >> 1) & 1, dx1 = rr & 1;
+  return (2 * dy1 + (s >> 1)) * 64 + 4 * x1l + 2 * dx1 + (s & 1);
+}
+// transposed 16x16x32 operand from a row-major LDS tile: lane (g, c), element j = X[row0 + 8 g + j][16 cb + c]
+template <bool DP>
+__device__ __forceinline__ bf16x8 tr_op(const char* smem, int row0, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int ch = 2 * cb + (pp >> 1);
+  const int r0 = row0 + 8 * g + q, r1 = r0 + 4;
+  const int o0 = (DP ? dp_off(r0, ch) : up_off(r0, ch)) + 8 * (pp & 1);
+  const int o1 = (DP ? dp_off(r1, ch) : up_off(r1, ch)) + 8 * (pp & 1);
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + o0));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + o1));
+  return cat8(a, b);
+}
+// B operand of one 16-row block: lane (g, c) = up1 row (row0 + c), k = 32 ks + 8 g .. + 7
+__device__ __forceinline__ void load_ublk(const bf16* __restrict__ up1, long long row0, bf16x8 (&ub)[2], int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) ub[ks] = *(const bf16x8*)(up1 + (row0 + c) * 64 + 32 * ks + 8 * g);
+}
+}  // namespace um
+
+// part_h fp32 [256][P * NS * 32] (per tile-in-prompt), part_w [grid][64][128], part_b [grid][32]
+template <int NS>
+__global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restrict__ up1, const bf16* __restrict__ w2,
+                                                            const float* __restrict__ b2,
+                                                            const float* __restrict__ hyper,
+                                                            const float* __restrict__ dmask, int ntiles, int P,
+                                                            bf16* __restrict__ dup1, float* __restrict__ part_h,
+                                                            float* __restrict__ part_w, float* __restrict__ part_b) {
+  using namespace um;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_red = (float*)(smem + S_DM + NS * 1024);  // [4 waves][NS * 32]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  // W2^T fragments for d up1 = dpre W2^T: fragment (m, kb), lane (g, c), element j = w2[k = 16 kb + c][n],
+  // n = 32 m + 16 (j >> 2) + 4 g + (j & 3) -- the lane's dpre registers of blocks 2m, 2m+1 in k-slot order
+  for (int e = tid; e < 16 * 64; e += 256) {
+    const int f = e >> 6, l = e & 63, m = f >> 2, kb = f & 3, lg = l >> 4, lc = l & 15;
+    const bf16* src = w2 + (16 * kb + lc) * 128 + 32 * m + 4 * lg;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = src[j], v[4 + j] = src[16 + j];
+    *(bf16x8*)(smem + S_W2T + 16 * e) = v;
+  }
+  // ConvT2 A fragments (nb, ks) in fragment order (read per tile: registers go to the d W2 accumulators)
+  for (int e = tid; e < 16 * 64; e += 256) {
+    const int f = e >> 6, l = e & 63, nb = f >> 1, ks = f & 1, lg = l >> 4, lc = l & 15;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = w2[(32 * ks + 8 * lg + j) * 128 + 16 * nb + lc];
+    *(bf16x8*)(smem + S_W2 + 16 * e) = v;
+  }
+  if (tid < 128) ((float*)(smem + S_BIAS))[tid] = b2[tid & 31];
+  f32x4 dwacc[4][2];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) dwacc[kb][0] = dwacc[kb][1] = (f32x4)0.0f;
+  float bacc[2][4];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bacc[hh][i] = 0.0f;
+
+  bf16x8 nxt[2];
+  float4 dnx[NS];
+  auto prefetch = [&](int Tn) {
+    load_ublk(up1, (long long)Tn * BROWS + 16 * w, nxt, lane);
+    if (tid < 64) {
+      const int p = Tn / BTILES_PER_P, y1 = (Tn >> 2) & 63, q = Tn & 3, yl = tid >> 4, x4 = (tid & 15) * 4;
+#pragma unroll
+      for (int t = 0; t < NS; ++t)
+        dnx[t] = *(const float4*)(dmask + (long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 64 * q + x4);
+    }
+  };
+  int T = blockIdx.x;
+  if (T < ntiles) prefetch(T);
+  for (; T < ntiles; T += gridDim.x) {
+    bf16x8 ub[2] = {nxt[0], nxt[1]};
+    float4 dcur[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) dcur[t] = dnx[t];
+    if (T + (int)gridDim.x < ntiles) prefetch(T + gridDim.x);
+    const int p = T / BTILES_PER_P;
+    const int rr = 16 * w + c;
+    __syncthreads();  // (A) the previous tile's LDS readers are done
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) *(bf16x8*)(smem + up_off(rr, 4 * ks + g)) = ub[ks];
+    if (tid < 64) {
+#pragma unroll
+      for (int t = 0; t < NS; ++t) *(float4*)(smem + S_DM + t * 1024 + tid * 16) = dcur[t];
+    }
+    f32x4 hy[NS][2];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) hy[t][hh] = *(const f32x4*)(hyper + (p * NS + t) * 32 + 16 * hh + 4 * g);
+    f32x4 acc[8];
+    {
+      f32x4 binit[8];
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) binit[nb] = *(const f32x4*)(smem + S_BIAS + 4 * (16 * nb + 4 * g));
+      bf16x8 wf[8][2];
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) wf[nb][ks] = *(const bf16x8*)(smem + S_W2 + 16 * ((2 * nb + ks) * 64 + lane));
+      convt2(wf, ub, binit, acc);
+    }
+    __syncthreads();  // (B) d masks staged
+    float dm[NS][4];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int dy2 = 0; dy2 < 2; ++dy2) {
+        const float2 v = *(const float2*)(smem + S_DM + t * 1024 + 4 * bpix_local(rr, 2 * dy2));
+        dm[t][2 * dy2] = v.x;
+        dm[t][2 * dy2 + 1] = v.y;
+      }
+    float hacc[NS][2][4];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hacc[t][hh][i] = 0.0f;
+    // elementwise per pair of 16-column blocks (2m, 2m+1) = one k-step of d up1 = dpre W2^T, accumulated at once
+    // (D[k][row], lane (g, c): row c, k = 16 kb + 4 g + i) so only one pair of dpre blocks is live
+    f32x4 da[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) da[kb] = (f32x4)0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      s16x4 dpk[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int nb = 2 * m + hh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float u, du;
+          gelu_both(acc[nb][i], u, du);
+          float d = 0.0f;
+#pragma unroll
+          for (int t = 0; t < NS; ++t) {
+            d = fmaf(dm[t][m], hy[t][hh][i], d);
+            hacc[t][hh][i] = fmaf(dm[t][m], u, hacc[t][hh][i]);
+          }
+          const float dp = d * du;
+          bacc[hh][i] += dp;
+          dpk[hh][i] = __builtin_bit_cast(short, (bf16)dp);
+        }
+        *(s16x4*)(smem + dp_off(rr, 2 * nb + (g >> 1)) + 8 * (g & 1)) = dpk[hh];
+      }
+      const bf16x8 bop = cat8(dpk[0], dpk[1]);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        da[kb] = mfma32(*(const bf16x8*)(smem + S_W2T + 16 * ((4 * m + kb) * 64 + lane)), bop, da[kb]);
+    }
+    {
+      const long long orow = (long long)T * BROWS + rr;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)da[kb][i];
+        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
+      }
+    }
+    // d hyper of this tile: sum over the 16 rows of each lane group (the 4 waves are summed after (C))
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = hacc[t][hh][i];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+          if (c == 0) s_red[w * NS * 32 + t * 32 + 16 * hh + 4 * g + i] = v;
+        }
+    __syncthreads();  // (C) dpre tile and d hyper rows complete
+    if (tid < NS * 32) {
+      const float v = s_red[tid] + s_red[NS * 32 + tid] + s_red[2 * NS * 32 + tid] + s_red[3 * NS * 32 + tid];
+      part_h[(long long)(T % BTILES_PER_P) * P * NS * 32 + p * NS * 32 + tid] = v;
+    }
+    // d W2 partial over the tile's 64 rows: wave w owns n blocks 2w, 2w+1; D[k][n], lane: k = 16 kb + 4 g + i, n = 16 nb + c
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bo[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bo[j] = tr_op<true>(smem, 32 * ks, 2 * w + j, lane);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const bf16x8 ao = tr_op<false>(smem, 32 * ks, kb, lane);
+        dwacc[kb][0] = mfma32(ao, bo[0], dwacc[kb][0]);
+        dwacc[kb][1] = mfma32(ao, bo[1], dwacc[kb][1]);
+      }
+    }
+  }
+  // per-workgroup partials of d W2 and d b2
+  float* pw = part_w + (long long)blockIdx.x * 8192;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pw[(16 * kb + 4 * g + i) * 128 + 16 * (2 * w + j) + c] = dwacc[kb][j][i];
+  __syncthreads();
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = bacc[hh][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (c == 0) s_red[w * 32 + 16 * hh + 4 * g + i] = v;
+    }
+  __syncthreads();
+  if (tid < 32) part_b[blockIdx.x * 32 + tid] = s_red[tid] + s_red[32 + tid] + s_red[64 + tid] + s_red[96 + tid];
+}
+
+int upmask_grid(int ntiles) { return ntiles < um::NWG ? ntiles : um::NWG; }
+}  // namespace
+
+extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
+                                    void* stream);
+
+extern "C" int octsam_upmask_fwd(const void* up1, const void* w2, const float* b2, const float* hyper, int32_t P,
+                                 int32_t ntok, float* masks, void* stream) {
+  OCTSAM_CHECK_ARG(up1 && w2 && b2 && hyper && masks && P > 0 && (ntok == 1 || ntok == 3),
+                   "octsam_upmask_fwd: bad args (ntok must be 1 or 3)");
+  OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)masks & 15) == 0,
+                   "octsam_upmask_fwd: up1, hyper and masks must be 16-B aligned");
+  const int ntiles = P * um::TILES_PER_P, grid = upmask_grid(ntiles);
+  hipStream_t s = (hipStream_t)stream;
+  if (ntok == 1)
+    hipLaunchKernelGGL(upmask_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, (const bf16*)up1, (const bf16*)w2, b2, hyper,
+                       ntiles, masks);
+  else
+    hipLaunchKernelGGL(upmask_fwd_kernel<3>, dim3(grid), dim3(256), 0, s, (const bf16*)up1, (const bf16*)w2, b2, hyper,
+                       ntiles, masks);
+  OCTSAM_LAUNCH_CHECK("octsam_upmask_fwd");
+  return 0;
+}
+
+extern "C" int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok) {
+  if (P <= 0 || ntok <= 0) return 0;
+  const long long grid = upmask_grid(P * um::BTILES_PER_P);
+  return (long long)um::BTILES_PER_P * P * ntok * 32 + grid * 8192 + grid * 32;
+}
+
+extern "C" int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper,
+                                 const float* dmask, int32_t P, int32_t ntok, void* dup1, float* dw2, float* db2,
+                                 float* dhyper, float* workspace, void* stream) {
+  OCTSAM_CHECK_ARG(up1 && w2 && b2 && hyper && dmask && dup1 && dw2 && db2 && dhyper && workspace && P > 0 &&
+                       (ntok == 1 || ntok == 3),
+                   "octsam_upmask_bwd: bad args (ntok must be 1 or 3)");
+  OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
+                       ((uintptr_t)dup1 & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
+                   "octsam_upmask_bwd: misaligned operand");
+  const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles);
+  float* part_h = workspace;
+  float* part_w = part_h + (long long)um::BTILES_PER_P * P * ntok * 32;
+  float* part_b = part_w + (long long)grid * 8192;
+  hipStream_t s = (hipStream_t)stream;
+  const int lds = um::S_DM + ntok * 1024 + 4 * ntok * 32 * 4;
+  if (ntok == 1)
+    hipLaunchKernelGGL(upmask_bwd_kernel<1>, dim3(grid), dim3(256), lds, s, (const bf16*)up1, (const bf16*)w2, b2,
+                       hyper, dmask, ntiles, P, (bf16*)dup1, part_h, part_w, part_b);
+  else
+    hipLaunchKernelGGL(upmask_bwd_kernel<3>, dim3(grid), dim3(256), lds, s, (const bf16*)up1, (const bf16*)w2, b2,
+                       hyper, dmask, ntiles, P, (bf16*)dup1, part_h, part_w, part_b);
+  OCTSAM_LAUNCH_CHECK("octsam_upmask_bwd");
+  int rc = octsam_splitk_reduce(part_h, dhyper, (int64_t)P * ntok * 32, um::BTILES_PER_P, 0.0f, stream);
+  if (!rc) rc = octsam_splitk_reduce(part_w, dw2, 8192, grid, 0.0f, stream);
+  if (!rc) rc = octsam_splitk_reduce(part_b, db2, 32, grid, 0.0f, stream);
+  return rc;
+}

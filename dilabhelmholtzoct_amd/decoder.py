@@ -535,8 +535,7 @@ class MaskDecoder(nn.Module):
                         torch.empty(P, self.num_mask_tokens, device=dev, dtype=f32), P)
         # ---- upscaling: ConvT(256->64) -> LN2d -> GELU -> ConvT(64->32) -> GELU (:519-521)
         b1 = self.Bf("upscale_conv1.bias").repeat(4)
-        b2 = self.Bf("upscale_conv2.bias").repeat(4)
-        s.up_b1, s.up_b2 = b1, b2
+        s.up_b1 = b1
         up1pre = torch.empty(RL, 4 * 64, device=dev, dtype=b16)
         K.gemm(keys_b, self.W("upscale_conv1.weight").t().contiguous(), M=RL, N=256, K=C, out=up1pre, bias=b1)
         up1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
@@ -545,14 +544,9 @@ class MaskDecoder(nn.Module):
         K.layernorm_fwd(up1pre, self.Bf("upscale_layer_norm.weight"), self.Bf("upscale_layer_norm.bias"), 1e-6, up1,
                         act=ACT_GELU, mean=mean, rstd=rstd)
         s.up1pre, s.up1, s.up_mean, s.up_rstd = up1pre, up1, mean, rstd
-        up2 = torch.empty(RL * 4, 128, device=dev, dtype=b16)
-        up2pre = torch.empty(RL * 4, 128, device=dev, dtype=b16)
-        K.gemm(up1, self.W("upscale_conv2.weight").t().contiguous(), M=RL * 4, N=128, K=64, out=up2, bias=b2,
-               act=ACT_GELU,
-               pre_out=up2pre)
-        s.up2, s.up2pre = up2, up2pre
+        # ConvT2 -> GELU -> masks = hyper . up2, fused (csrc/upmask.hip): up2 is never stored
         masks = torch.empty(P, nsel, 256, 256, device=dev, dtype=f32)
-        K.mask_dot_fwd(up2, hyper, P, nsel, masks)
+        K.upmask_fwd(up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), hyper, P, nsel, masks)
         iou_sel = iou[:, sel[0]:sel[-1] + 1].contiguous()  # sel is a contiguous range (slice: capturable)
         return masks.view(B, N, nsel, 256, 256), iou_sel.view(B, N, nsel), s
 
@@ -567,17 +561,11 @@ class MaskDecoder(nn.Module):
         G.zero_()
         nsel = len(s.sel)
         dm = dmasks.reshape(P, nsel, 65536).contiguous().float()
-        # ---- mask head
-        dup2pre = torch.empty(RL * 4, 128, device=dev, dtype=b16)
-        dhyper = torch.empty(P * nsel * 32, device=dev, dtype=f32)
-        K.mask_dot_bwd(s.up2, s.up2pre, s.hyper, P, nsel, dm, dup2pre, dhyper)
-        dhyper = dhyper.view(P, nsel, 32)
-        # ConvT2: y[M4, (dy,dx,co2)] = up1[M4, 64] @ W2s[64, 128]
+        # ---- mask head + ConvT2 (+ GELU), fused: recomputes the ConvT2 product from up1
+        dhyper = torch.empty(P, nsel, 32, device=dev, dtype=f32)
         dup1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
-        W2s = self.W("upscale_conv2.weight")
-        K.gemm(dup2pre, W2s, M=RL * 4, N=64, K=128, out=dup1, b_mode=0)
-        self._dw(s.up1, dup2pre, RL * 4, self.G("upscale_conv2.weight"), ldy=64, ldx=128)
-        K.colsum(dup2pre, RL * 16, 32, self.G("upscale_conv2.bias"))
+        K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel, dup1,
+                     self.G("upscale_conv2.weight"), self.G("upscale_conv2.bias"), dhyper)
         # LN2d + GELU
         dup1pre = torch.empty(RL * 4, 64, device=dev, dtype=b16)
         K.layernorm_bwd(dup1, s.up1pre, s.up_mean, s.up_rstd, self.Bf("upscale_layer_norm.weight"),

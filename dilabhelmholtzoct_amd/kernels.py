@@ -233,6 +233,23 @@ def mask_dot_bwd(up2, up2pre, hyper, P, ntok, dmask, dup2pre, dhyper):
     return dup2pre, dhyper
 
 
+def upmask_fwd(up1, w2, b2, hyper, P, ntok, masks):
+    """Fused ConvT2 + GELU + mask head (octsam_upmask_fwd): masks [P, ntok, 256, 256] fp32."""
+    _require_cuda(up1, w2, b2, hyper, masks)
+    _lib.call("octsam_upmask_fwd", ptr(up1), ptr(w2), ptr(b2), ptr(hyper), P, ntok, ptr(masks))
+    return masks
+
+
+def upmask_bwd(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper):
+    """Backward of upmask_fwd: writes d up1 (bf16) and overwrites d w2, d b2, d hyper (fp32)."""
+    _require_cuda(up1, w2, b2, hyper, dmask, dup1, dw2, db2, dhyper)
+    n = _lib.load().octsam_upmask_bwd_workspace(P, ntok)
+    ws = torch.empty(n, device=up1.device, dtype=torch.float32)
+    _lib.call("octsam_upmask_bwd", ptr(up1), ptr(w2), ptr(b2), ptr(hyper), ptr(dmask), P, ntok, ptr(dup1), ptr(dw2),
+              ptr(db2), ptr(dhyper), ptr(ws))
+    return dup1
+
+
 def adam(params, grads, exp_avg, exp_avg_sq, *, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt,
          params_bf16=None):
     _lib.call("octsam_adam", ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), params.numel(), beta1, beta2,

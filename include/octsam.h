@@ -199,6 +199,22 @@ int octsam_mask_dot_fwd(const void* up2, const float* hyper, int32_t P, int32_t 
 int octsam_mask_dot_bwd(const void* up2, const void* up2pre, const float* hyper, int32_t P, int32_t ntok,
                         const float* dmask, void* dup2pre, float* partials, void* stream);
 
+/* Fused upscaling tail + mask head (hf:modeling_sam.py:519-542: the second ConvTranspose2d, its GELU
+ * and masks = hyper_in @ upscaled_embedding; replaces octsam_gemm (conv2) + octsam_mask_dot_* in the
+ * training step): the 32-channel 256x256 upscaled embedding is never stored.
+ * up1 bf16 [P*16384, 64] (LN+GELU output of the first ConvTranspose2d, blocked row order as above);
+ * w2 bf16 [64, 128] = ConvT2 weight [in][(dy2, dx2, c)]; b2 fp32 [32]; hyper fp32 [P, ntok, 32];
+ * ntok = 1 or 3; masks fp32 [P, ntok, 256, 256].
+ * Backward recomputes the ConvT2 product and writes d up1 (bf16 [P*16384, 64]) and, overwriting,
+ * d w2 fp32 [64, 128], d b2 fp32 [32], d hyper fp32 [P, ntok, 32] (fixed-order reductions).
+ * workspace: octsam_upmask_bwd_workspace(P, ntok) floats, 16-B aligned. */
+int octsam_upmask_fwd(const void* up1, const void* w2, const float* b2, const float* hyper, int32_t P, int32_t ntok,
+                      float* masks, void* stream);
+int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok);
+int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask,
+                      int32_t P, int32_t ntok, void* dup1, float* dw2, float* db2, float* dhyper, float* workspace,
+                      void* stream);
+
 /* ---------------------------------------------------------------- post-processing + losses
  * octsam_postproc_fwd: ref:octsam/models/training_utils.py:57-59 — lowres fp32 [M,S,S] -> bilinear to
  *   mid x mid (align_corners=False) -> crop [:crop_h,:crop_w] -> bilinear to out_h x out_w, fused,
