@@ -66,6 +66,7 @@ _SIGNATURES = {
                                        c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "octsam_patchify_bf16": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_dec_tok_attn_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                           c_void_p]),
     "octsam_dec_tok_attn_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
@@ -86,6 +87,7 @@ _SIGNATURES = {
                                       c_void_p, c_void_p]),
     "octsam_upmask_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "octsam_upmask_bwd_workspace": (c_int64, [c_int32, c_int32]),
+    "octsam_upmask_set_grid": (None, [c_int32, c_int32]),
     "octsam_upmask_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_postproc_fwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

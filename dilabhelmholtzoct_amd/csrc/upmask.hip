@@ -69,24 +69,36 @@ __device__ __forceinline__ int pix_local(int rr, int s) {
   const int x1l = rr >> 2, dy1 = (rr >> 1) & 1, dx1 = rr & 1;
   return (2 * dy1 + (s >> 1)) * 128 + 4 * x1l + 2 * dx1 + (s & 1);
 }
-// GELU (erf form) and its derivative from one shared erf / exp evaluation (A&S 7.1.26, |err| <= 1.5e-7)
-__device__ __forceinline__ void gelu_both(float x, float& y, float& dy) {
-  const float u = x * 0.70710678118654752f, au = fabsf(u);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, au, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = __expf(-au * au);  // = exp(-x^2 / 2)
-  const float phi2 = 1.0f + copysignf(1.0f - p * t * e, u);
-  y = 0.5f * x * phi2;
-  dy = fmaf(x * 0.3989422804014327f, e, 0.5f * phi2);
+// GELU (erf form) and its derivative on two values at once (packed f32: v_pk_fma / v_pk_mul / v_pk_add, the
+// kernels are VALU-bound), one shared erf / exp evaluation (A&S 7.1.26, |err| <= 1.5e-7)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <bool GRAD>
+__device__ __forceinline__ void gelu2(f32x2 x, f32x2& y, f32x2& dy) {
+  const f32x2 u = x * 0.70710678118654752f;
+  const f32x2 au = __builtin_elementwise_abs(u);
+  const f32x2 den = fma2(au, (f32x2)0.3275911f, (f32x2)1.0f);
+  f32x2 t;
+  t.x = __builtin_amdgcn_rcpf(den.x);
+  t.y = __builtin_amdgcn_rcpf(den.y);
+  f32x2 p = fma2((f32x2)1.061405429f, t, (f32x2)-1.453152027f);
+  p = fma2(p, t, (f32x2)1.421413741f);
+  p = fma2(p, t, (f32x2)-0.284496736f);
+  p = fma2(p, t, (f32x2)0.254829592f);
+  const f32x2 q = (au * au) * -1.4426950408889634f;
+  f32x2 e;  // exp(-x^2 / 2)
+  e.x = __builtin_amdgcn_exp2f(q.x);
+  e.y = __builtin_amdgcn_exp2f(q.y);
+  const f32x2 r = fma2(-(p * t), e, (f32x2)1.0f);
+  const f32x2 phi2 = __builtin_elementwise_copysign(r, u) + 1.0f;
+  y = (x * 0.5f) * phi2;
+  if constexpr (GRAD) dy = fma2(x * 0.3989422804014327f, e, phi2 * 0.5f);
 }
 }  // namespace um
 
 // grid: min(NWG, tiles) persistent workgroups of 256 threads; masks fp32 [P, NS, 256, 256]
 template <int NS>
-__global__ __launch_bounds__(256, 2) void upmask_fwd_kernel(const bf16* __restrict__ up1, const bf16* __restrict__ w2,
+__global__ __launch_bounds__(256, 3) void upmask_fwd_kernel(const bf16* __restrict__ up1, const bf16* __restrict__ w2,
                                                             const float* __restrict__ b2,
                                                             const float* __restrict__ hyper, int ntiles,
                                                             float* __restrict__ masks) {
@@ -100,20 +112,21 @@ __global__ __launch_bounds__(256, 2) void upmask_fwd_kernel(const bf16* __restri
   for (int nb = 0; nb < 8; ++nb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) binit[nb][i] = b2[(16 * nb + 4 * g + i) & 31];
-  bf16x8 nxt[2][2];
+  // Every global access in the loop is unconditional (the last prefetch re-reads a valid tile) and the
+  // prefetch alternates between two register sets (the loop is unrolled by two), so the compiler's vmcnt
+  // bookkeeping is exact and no copy of the prefetched registers waits inside the tile that issued it.
+  bf16x8 fa[2][2], fb[2][2];
   int T = blockIdx.x;
-  if (T < ntiles) load_ufrag(up1, (long long)T * ROWS + 32 * w, nxt, lane);
-  for (int it = 0; T < ntiles; T += gridDim.x, ++it) {
-    bf16x8 uf[2][2];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) uf[rb][0] = nxt[rb][0], uf[rb][1] = nxt[rb][1];
-    if (T + (int)gridDim.x < ntiles) load_ufrag(up1, (long long)(T + gridDim.x) * ROWS + 32 * w, nxt, lane);
+  if (T >= ntiles) return;
+  load_ufrag(up1, (long long)T * ROWS + 32 * w, fa, lane);
+  auto step = [&](const bf16x8 (&uf)[2][2], bf16x8 (&nx)[2][2], int T, int it) {
     const int p = T / TILES_PER_P, y1 = (T >> 1) & 63, h = T & 1;
     f32x4 hy[NS][2];
 #pragma unroll
     for (int t = 0; t < NS; ++t)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) hy[t][hh] = *(const f32x4*)(hyper + (p * NS + t) * 32 + 16 * hh + 4 * g);
+    load_ufrag(up1, (long long)min(T + (int)gridDim.x, ntiles - 1) * ROWS + 32 * w, nx, lane);
     float* sm = smask[it & 1];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
@@ -127,10 +140,14 @@ __global__ __launch_bounds__(256, 2) void upmask_fwd_kernel(const bf16* __restri
 #pragma unroll
       for (int nb = 0; nb < 8; ++nb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float u = gelu_fast(acc[nb][i]);
+        for (int i = 0; i < 4; i += 2) {
+          f32x2 u, du;
+          gelu2<false>(f32x2{acc[nb][i], acc[nb][i + 1]}, u, du);
 #pragma unroll
-          for (int t = 0; t < NS; ++t) m[t][nb >> 1] = fmaf(hy[t][nb & 1][i], u, m[t][nb >> 1]);
+          for (int t = 0; t < NS; ++t) {
+            const f32x2 pr = f32x2{hy[t][nb & 1][i], hy[t][nb & 1][i + 1]} * u;
+            m[t][nb >> 1] += pr.x + pr.y;
+          }
         }
       // reduce-scatter over the 4 lane groups: group g ends with the full sum of sub-pixel s = g
       const int rr = 32 * w + 16 * rb + c;
@@ -147,11 +164,18 @@ __global__ __launch_bounds__(256, 2) void upmask_fwd_kernel(const bf16* __restri
       }
     }
     __syncthreads();  // (double-buffered staging: the buffer written next was last read before this barrier)
-    for (int e = tid; e < NS * 128; e += 256) {
-      const int t = e >> 7, yl = (e >> 5) & 3, x4 = (e & 31) * 4;
-      *(float4*)(masks + ((long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 128 * h + x4)) =
-          *(const float4*)(sm + t * 512 + yl * 128 + x4);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {  // 2 floats per thread and mask: the [4][128] block, 512-B row runs
+      const int yl = tid >> 6, x2 = (tid & 63) * 2;
+      *(float2*)(masks + ((long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 128 * h + x2)) =
+          *(const float2*)(sm + t * 512 + yl * 128 + x2);
     }
+  };
+  for (int it = 0;; it += 2) {
+    step(fa, fb, T, it);
+    if ((T += gridDim.x) >= ntiles) break;
+    step(fb, fa, T, it + 1);
+    if ((T += gridDim.x) >= ntiles) break;
   }
 }
 
@@ -204,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
   using namespace um;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_red = (float*)(smem + S_DM + NS * 1024);  // [4 waves][NS * 32]
+  float* scratch = part_b + gridDim.x * 32 + blockIdx.x * 256;  // sink of the idle threads' partial stores
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   // W2^T fragments for d up1 = dpre W2^T: fragment (m, kb), lane (g, c), element j = w2[k = 16 kb + c][n],
   // n = 32 m + 16 (j >> 2) + 4 g + (j & 3) -- the lane's dpre registers of blocks 2m, 2m+1 in k-slot order
@@ -233,39 +258,32 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) bacc[hh][i] = 0.0f;
 
-  bf16x8 nxt[2];
-  float4 dnx[NS];
-  auto prefetch = [&](int Tn) {
-    load_ublk(up1, (long long)Tn * BROWS + 16 * w, nxt, lane);
-    if (tid < 64) {
-      const int p = Tn / BTILES_PER_P, y1 = (Tn >> 2) & 63, q = Tn & 3, yl = tid >> 4, x4 = (tid & 15) * 4;
+  // Unconditional global accesses and alternating prefetch buffers, as in the forward.
+  bf16x8 ua[2], ubb[2];
+  float da_[NS], db_[NS];
+  auto prefetch = [&](int Tn, bf16x8 (&nu)[2], float (&nd)[NS]) {  // up1 block + the tile's d masks
+    load_ublk(up1, (long long)Tn * BROWS + 16 * w, nu, lane);      // ([NS][4][64]: one float per thread and mask)
+    const int p = Tn / BTILES_PER_P, y1 = (Tn >> 2) & 63, q = Tn & 3, yl = tid >> 6, x = tid & 63;
 #pragma unroll
-      for (int t = 0; t < NS; ++t)
-        dnx[t] = *(const float4*)(dmask + (long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 64 * q + x4);
-    }
+    for (int t = 0; t < NS; ++t) nd[t] = dmask[(long long)(p * NS + t) * 65536 + (4 * y1 + yl) * 256 + 64 * q + x];
   };
   int T = blockIdx.x;
-  if (T < ntiles) prefetch(T);
-  for (; T < ntiles; T += gridDim.x) {
-    bf16x8 ub[2] = {nxt[0], nxt[1]};
-    float4 dcur[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) dcur[t] = dnx[t];
-    if (T + (int)gridDim.x < ntiles) prefetch(T + gridDim.x);
+  if (T >= ntiles) return;
+  prefetch(T, ua, da_);
+  auto step = [&](const bf16x8 (&ub)[2], const float (&dcur)[NS], bf16x8 (&nu)[2], float (&nd)[NS], int T) {
     const int p = T / BTILES_PER_P;
     const int rr = 16 * w + c;
-    __syncthreads();  // (A) the previous tile's LDS readers are done
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) *(bf16x8*)(smem + up_off(rr, 4 * ks + g)) = ub[ks];
-    if (tid < 64) {
-#pragma unroll
-      for (int t = 0; t < NS; ++t) *(float4*)(smem + S_DM + t * 1024 + tid * 16) = dcur[t];
-    }
     f32x4 hy[NS][2];
 #pragma unroll
     for (int t = 0; t < NS; ++t)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) hy[t][hh] = *(const f32x4*)(hyper + (p * NS + t) * 32 + 16 * hh + 4 * g);
+    prefetch(min(T + (int)gridDim.x, ntiles - 1), nu, nd);
+    __syncthreads();  // (A) the previous tile's LDS readers are done
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) *(bf16x8*)(smem + up_off(rr, 4 * ks + g)) = ub[ks];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) ((float*)(smem + S_DM + t * 1024))[tid] = dcur[t];
     f32x4 acc[8];
     {
       f32x4 binit[8];
@@ -307,18 +325,23 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
       for (int hh = 0; hh < 2; ++hh) {
         const int nb = 2 * m + hh;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float u, du;
-          gelu_both(acc[nb][i], u, du);
-          float d = 0.0f;
+        for (int i = 0; i < 4; i += 2) {
+          f32x2 u, du;
+          gelu2<true>(f32x2{acc[nb][i], acc[nb][i + 1]}, u, du);
+          f32x2 d = (f32x2)0.0f;
 #pragma unroll
           for (int t = 0; t < NS; ++t) {
-            d = fmaf(dm[t][m], hy[t][hh][i], d);
-            hacc[t][hh][i] = fmaf(dm[t][m], u, hacc[t][hh][i]);
+            const f32x2 dmv = (f32x2)dm[t][m];
+            d = fma2(dmv, f32x2{hy[t][hh][i], hy[t][hh][i + 1]}, d);
+            const f32x2 h2 = fma2(dmv, u, f32x2{hacc[t][hh][i], hacc[t][hh][i + 1]});
+            hacc[t][hh][i] = h2.x;
+            hacc[t][hh][i + 1] = h2.y;
           }
-          const float dp = d * du;
-          bacc[hh][i] += dp;
-          dpk[hh][i] = __builtin_bit_cast(short, (bf16)dp);
+          const f32x2 dp = d * du;
+          bacc[hh][i] += dp.x;
+          bacc[hh][i + 1] += dp.y;
+          dpk[hh][i] = __builtin_bit_cast(short, (bf16)dp.x);
+          dpk[hh][i + 1] = __builtin_bit_cast(short, (bf16)dp.y);
         }
         *(s16x4*)(smem + dp_off(rr, 2 * nb + (g >> 1)) + 8 * (g & 1)) = dpk[hh];
       }
@@ -350,9 +373,12 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
           if (c == 0) s_red[w * NS * 32 + t * 32 + 16 * hh + 4 * g + i] = v;
         }
     __syncthreads();  // (C) dpre tile and d hyper rows complete
-    if (tid < NS * 32) {
-      const float v = s_red[tid] + s_red[NS * 32 + tid] + s_red[2 * NS * 32 + tid] + s_red[3 * NS * 32 + tid];
-      part_h[(long long)(T % BTILES_PER_P) * P * NS * 32 + p * NS * 32 + tid] = v;
+    {
+      const int j = tid < NS * 32 ? tid : 0;
+      const float v = s_red[j] + s_red[NS * 32 + j] + s_red[2 * NS * 32 + j] + s_red[3 * NS * 32 + j];
+      float* dst = tid < NS * 32 ? part_h + (long long)(T % BTILES_PER_P) * P * NS * 32 + p * NS * 32 + tid
+                                 : scratch + tid;
+      *dst = v;
     }
     // d W2 partial over the tile's 64 rows: wave w owns n blocks 2w, 2w+1; D[k][n], lane: k = 16 kb + 4 g + i, n = 16 nb + c
 #pragma unroll
@@ -367,7 +393,14 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
         dwacc[kb][1] = mfma32(ao, bo[1], dwacc[kb][1]);
       }
     }
+  };
+  for (;;) {
+    step(ua, da_, ubb, db_, T);
+    if ((T += gridDim.x) >= ntiles) break;
+    step(ubb, db_, ua, da_, T);
+    if ((T += gridDim.x) >= ntiles) break;
   }
+
   // per-workgroup partials of d W2 and d b2
   float* pw = part_w + (long long)blockIdx.x * 8192;
 #pragma unroll
@@ -390,8 +423,14 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
   if (tid < 32) part_b[blockIdx.x * 32 + tid] = s_red[tid] + s_red[32 + tid] + s_red[64 + tid] + s_red[96 + tid];
 }
 
-int upmask_grid(int ntiles) { return ntiles < um::NWG ? ntiles : um::NWG; }
+int g_fwd_grid = 768, g_bwd_grid = um::NWG;  // persistent grids (octsam_upmask_set_grid: tuning)
+int upmask_grid(int ntiles, int cap) { return ntiles < cap ? ntiles : cap; }
 }  // namespace
+
+extern "C" void octsam_upmask_set_grid(int32_t fwd, int32_t bwd) {
+  if (fwd > 0) g_fwd_grid = fwd;
+  if (bwd > 0) g_bwd_grid = bwd < um::NWG ? bwd : um::NWG;  // (the workspace is sized for NWG partials)
+}
 
 extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
                                     void* stream);
@@ -402,7 +441,7 @@ extern "C" int octsam_upmask_fwd(const void* up1, const void* w2, const float* b
                    "octsam_upmask_fwd: bad args (ntok must be 1 or 3)");
   OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)masks & 15) == 0,
                    "octsam_upmask_fwd: up1, hyper and masks must be 16-B aligned");
-  const int ntiles = P * um::TILES_PER_P, grid = upmask_grid(ntiles);
+  const int ntiles = P * um::TILES_PER_P, grid = upmask_grid(ntiles, g_fwd_grid);
   hipStream_t s = (hipStream_t)stream;
   if (ntok == 1)
     hipLaunchKernelGGL(upmask_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, (const bf16*)up1, (const bf16*)w2, b2, hyper,
@@ -416,8 +455,8 @@ extern "C" int octsam_upmask_fwd(const void* up1, const void* w2, const float* b
 
 extern "C" int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok) {
   if (P <= 0 || ntok <= 0) return 0;
-  const long long grid = upmask_grid(P * um::BTILES_PER_P);
-  return (long long)um::BTILES_PER_P * P * ntok * 32 + grid * 8192 + grid * 32;
+  const long long grid = upmask_grid(P * um::BTILES_PER_P, um::NWG);
+  return (long long)um::BTILES_PER_P * P * ntok * 32 + grid * 8192 + grid * 32 + grid * 256;
 }
 
 extern "C" int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper,
@@ -429,7 +468,7 @@ extern "C" int octsam_upmask_bwd(const void* up1, const void* w2, const float* b
   OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
                        ((uintptr_t)dup1 & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
                    "octsam_upmask_bwd: misaligned operand");
-  const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles);
+  const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles, g_bwd_grid);
   float* part_h = workspace;
   float* part_w = part_h + (long long)um::BTILES_PER_P * P * ntok * 32;
   float* part_b = part_w + (long long)grid * 8192;

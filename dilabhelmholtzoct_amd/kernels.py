@@ -141,6 +141,13 @@ def axpby(a, b, out, *, alpha=1.0, beta=1.0, b_period=0, out2_f32=None, n=None):
     return out
 
 
+def patchify_bf16(px, out):
+    """pixel_values fp32 [B, 3, 1024, 1024] -> patch rows bf16 [B*4096, 768] (k = c, ky, kx)."""
+    _require_cuda(px, out)
+    _lib.call("octsam_patchify_bf16", ptr(px), px.shape[0], ptr(out))
+    return out
+
+
 def cast_bf16(x, out):
     _lib.call("octsam_cast_bf16", ptr(x), ptr(out), x.numel())
     return out

@@ -153,8 +153,9 @@ class VisionEncoder(nn.Module):
         heads = cfg.num_attention_heads
         pe = self.patch_embed.projection
         x = torch.empty(M, D, device=dev, dtype=torch.float32)
-        K.gemm(px, self._w("patch.w", pe.weight, lambda t: t.reshape(D, -1)), M=M, N=D, K=3 * 256, out=x,
-               a_mode=2, bias=self._wf("patch.b", pe.bias), residual=self._wf("pos", self.pos_embed,
+        patches = K.patchify_bf16(px, torch.empty(M, 3 * 256, device=dev, dtype=torch.bfloat16))
+        K.gemm(patches, self._w("patch.w", pe.weight, lambda t: t.reshape(D, -1)), M=M, N=D, K=3 * 256, out=x,
+               bias=self._wf("patch.b", pe.bias), residual=self._wf("pos", self.pos_embed,
                                                                                    lambda t: t.reshape(L, D)),
                r_remap=(L, B))
         xn = torch.empty(M, D, device=dev, dtype=torch.bfloat16)

@@ -160,6 +160,9 @@ int octsam_group_sum(const void* in, int64_t ld_in, int32_t cols, int32_t groups
                      void* out, void* stream);
 /* bf16 copy of an fp32 buffer */
 int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+/* Patch-embedding operand: pixel_values fp32 [B, 3, 1024, 1024] -> bf16 [B*4096, 768], row = (b, py, px),
+ * k = (c, ky, kx) (= Conv2d(3, D, 16, 16) weight.reshape(D, 768) order); replaces the gathered a_mode 2. */
+int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream);
 
 /* ---------------------------------------------------------------- mask decoder attention cores
  * SamAttention core softmax(q k^T / sqrt(dh)) v (hf:modeling_sam.py:231-270) for the three shapes of
@@ -211,6 +214,8 @@ int octsam_mask_dot_bwd(const void* up2, const void* up2pre, const float* hyper,
 int octsam_upmask_fwd(const void* up1, const void* w2, const float* b2, const float* hyper, int32_t P, int32_t ntok,
                       float* masks, void* stream);
 int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok);
+/* tuning: persistent grid sizes of the two kernels (defaults 768 / 512; the backward is capped at 512) */
+void octsam_upmask_set_grid(int32_t fwd, int32_t bwd);
 int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask,
                       int32_t P, int32_t ntok, void* dup1, float* dw2, float* db2, float* dhyper, float* workspace,
                       void* stream);

@@ -133,3 +133,15 @@ def test_vit_attention_deterministic(cuda, side, nseq):
         kernels.vit_attention(qkv, o, Rh, Rw, nseq=nseq, side=side, heads=12)
         outs.append(o)
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+def test_patchify_bf16(cuda):
+    """Patch-embedding operand: rows (b, patch row, patch col), k = (c, ky, kx), bf16-rounded pixels."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(12)
+    B = 2
+    px = torch.randn(B, 3, 1024, 1024, generator=g).to(cuda)
+    out = torch.empty(B * 4096, 768, device=cuda, dtype=torch.bfloat16)
+    kernels.patchify_bf16(px, out)
+    ref = px.view(B, 3, 64, 16, 64, 16).permute(0, 2, 4, 1, 3, 5).reshape(B * 4096, 768).to(torch.bfloat16)
+    assert torch.equal(out, ref)
