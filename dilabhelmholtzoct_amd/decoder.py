@@ -572,7 +572,9 @@ class MaskDecoder(nn.Module):
                         self.Bf("upscale_layer_norm.bias"), dup1pre, act=ACT_GELU,
                         dw=self.G("upscale_layer_norm.weight"), db=self.G("upscale_layer_norm.bias"))
         # ConvT1: y[RL, 256] = keys2[RL, 256] @ W1s[256, 256]
-        dkeys = torch.empty(RL, C, device=dev, dtype=f32)
+        # the image-side keys gradient stream is bf16 (as under the reference's bf16 autocast): it is written,
+        # read-modify-written by each block's projection backward and read by LayerNorm4's backward per block
+        dkeys = torch.empty(RL, C, device=dev, dtype=b16)
         K.gemm(dup1pre, self.W("upscale_conv1.weight"), M=RL, N=C, K=256, out=dkeys, b_mode=0)
         self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256)
         K.colsum(dup1pre, RL * 4, 64, self.G("upscale_conv1.bias"))
@@ -618,16 +620,12 @@ class MaskDecoder(nn.Module):
             # LN4 on keys
             x4, mean4, rstd4, _ = ls.ln4
             ds4_b = torch.empty(RL, C, device=dev, dtype=b16)
-            if li > 0:
-                dkeys_in = torch.empty(RL, C, device=dev, dtype=f32)
-                K.layernorm_bwd(dkeys, x4, mean4, rstd4, self.Bf(pre + "layer_norm4.weight"),
-                                self.Bf(pre + "layer_norm4.bias"), dkeys_in, dx2_bf16=ds4_b,
-                                dw=self.G(pre + "layer_norm4.weight"), db=self.G(pre + "layer_norm4.bias"))
-            else:
-                dkeys_in = None
-                K.layernorm_bwd(dkeys, x4, mean4, rstd4, self.Bf(pre + "layer_norm4.weight"),
-                                self.Bf(pre + "layer_norm4.bias"), ds4_b,
-                                dw=self.G(pre + "layer_norm4.weight"), db=self.G(pre + "layer_norm4.bias"))
+            K.layernorm_bwd(dkeys, x4, mean4, rstd4, self.Bf(pre + "layer_norm4.weight"),
+                            self.Bf(pre + "layer_norm4.bias"), ds4_b,
+                            dw=self.G(pre + "layer_norm4.weight"), db=self.G(pre + "layer_norm4.bias"))
+            # d keys_in = d s4 (residual) + the block's image-side projection gradients, accumulated in place
+            # once every reader of d s4 (out_proj backward) has run
+            dkeys_in = ds4_b if li > 0 else None
             # s4 = keys_in + i2t_out @ Wo^T + bo
             dio_b = torch.empty(RL, CI, device=dev, dtype=b16)
             self._lin_bwd(ds4_b, ls.i2t_o_b, i2t + "out_proj.weight", i2t + "out_proj.bias", RL, dx_out=dio_b)
