@@ -56,53 +56,88 @@ __device__ __forceinline__ float stage1(const float* __restrict__ x, const PP& p
   return a.l0 * (b.l0 * r0[b.i0] + b.l1 * r0[b.i1]) + a.l1 * (b.l0 * r1[b.i0] + b.l1 * r1[b.i1]);
 }
 
-// out[m][i][j] and Dice partials: part[m][blk][3] = (sum p*t, sum t, sum p)
+// out[m][i][j] and Dice partials: part[m][blk][3] = (sum p*t, sum t, sum p), blk = group of 4 output rows.
+// One workgroup per (map, 4 output rows): the contiguous range of low-res rows those rows need (<= 8, host-
+// checked) is staged in LDS with coalesced float4 loads, every one of the 16 taps
+// of an output pixel is an LDS read (the global gather version was address-bound), and each column's
+// stage-2 / stage-1 coordinates are computed once for the 4 rows.
+constexpr int PP_ROWS = 4, PP_LRMAX = 16;
 __global__ __launch_bounds__(256) void postproc_fwd_kernel(const float* __restrict__ low, PP pp,
                                                            float* __restrict__ out, const uint8_t* __restrict__ gt,
                                                            float* __restrict__ part) {
-  const int m = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) float rows[PP_LRMAX][256];
+  __shared__ float red[3][4];
+  const int m = blockIdx.y, i0 = blockIdx.x * PP_ROWS, tid = threadIdx.x;
+  const int nr = min(PP_ROWS, pp.oh - i0);
   const float* x = low + (long long)m * pp.S * pp.S;
-  const long long npix = (long long)pp.oh * pp.ow;
+  // low-res row range of the group: rows are monotone in i, so the first row's lowest and the last row's
+  // highest source bound it
+  const int lo = lin_acf(lin_acf(i0, pp.ch, pp.s2h).i0, pp.S, pp.s1).i0;
+  for (int e = tid; e < PP_LRMAX * 64; e += 256) {
+    const int r = e >> 6, c4 = (e & 63) * 4;
+    if (c4 < pp.S && lo + r < pp.S) *(float4*)&rows[r][c4] = *(const float4*)(x + (long long)(lo + r) * pp.S + c4);
+  }
+  __syncthreads();
   float si = 0.0f, st = 0.0f, sp = 0.0f;
-  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < npix; e += (long long)gridDim.x * 256) {
-    int i = (int)(e / pp.ow), j = (int)(e % pp.ow);
-    Lin h = lin_acf(i, pp.ch, pp.s2h), w = lin_acf(j, pp.cw, pp.s2w);
-    float v00 = stage1(x, pp, h.i0, w.i0), v01 = stage1(x, pp, h.i0, w.i1);
-    float v10 = stage1(x, pp, h.i1, w.i0), v11 = stage1(x, pp, h.i1, w.i1);
-    float v = h.l0 * (w.l0 * v00 + w.l1 * v01) + h.l1 * (w.l0 * v10 + w.l1 * v11);
-    out[(long long)m * npix + e] = v;
-    if (gt) {
-      float t = (float)gt[(long long)m * npix + e];
-      float p = 1.0f / (1.0f + __expf(-v));
-      si += p * t;
-      st += t;
-      sp += p;
+  Lin hs[PP_ROWS], a0s[PP_ROWS], a1s[PP_ROWS];  // row coordinates, once per row
+#pragma unroll
+  for (int r = 0; r < PP_ROWS; ++r) {
+    hs[r] = lin_acf(min(i0 + r, pp.oh - 1), pp.ch, pp.s2h);
+    a0s[r] = lin_acf(hs[r].i0, pp.S, pp.s1);
+    a1s[r] = lin_acf(hs[r].i1, pp.S, pp.s1);
+  }
+  for (int j = tid; j < pp.ow; j += 256) {
+    const Lin w = lin_acf(j, pp.cw, pp.s2w);
+    const Lin b0 = lin_acf(w.i0, pp.S, pp.s1), b1 = lin_acf(w.i1, pp.S, pp.s1);
+#pragma unroll
+    for (int r = 0; r < PP_ROWS; ++r) {
+      if (r >= nr) break;
+      const int i = i0 + r;
+      const Lin h = hs[r], a0 = a0s[r], a1 = a1s[r];
+      auto st1 = [&](const Lin& a, const Lin& bb) {
+        const float* ra = rows[a.i0 - lo];
+        const float* rb = rows[a.i1 - lo];
+        return a.l0 * (bb.l0 * ra[bb.i0] + bb.l1 * ra[bb.i1]) + a.l1 * (bb.l0 * rb[bb.i0] + bb.l1 * rb[bb.i1]);
+      };
+      const float v00 = st1(a0, b0), v01 = st1(a0, b1), v10 = st1(a1, b0), v11 = st1(a1, b1);
+      const float v = h.l0 * (w.l0 * v00 + w.l1 * v01) + h.l1 * (w.l0 * v10 + w.l1 * v11);
+      const long long o = ((long long)m * pp.oh + i) * pp.ow + j;
+      out[o] = v;
+      if (gt) {
+        const float t = (float)gt[o];
+        const float pr = 1.0f / (1.0f + __expf(-v));
+        si += pr * t;
+        st += t;
+        sp += pr;
+      }
     }
   }
   if (!gt) return;
-  __shared__ float red[3][4];
   si = wave_sum(si); st = wave_sum(st); sp = wave_sum(sp);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = tid >> 6, lane = tid & 63;
   if (lane == 0) { red[0][wave] = si; red[1][wave] = st; red[2][wave] = sp; }
   __syncthreads();
-  if (threadIdx.x < 3) {
-    float s = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
-    part[((long long)m * gridDim.x + blockIdx.x) * 3 + threadIdx.x] = s;
-  }
+  if (tid < 3)
+    part[((long long)m * gridDim.x + blockIdx.x) * 3 + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
 }
 
 // per-map dice sums -> dice loss per map, and the per-map gradient coefficients
 // coef[m] = (c1, c2): d(mean dice)/dx = (c1 * t + c2) * p (1 - p)
-__global__ void dice_reduce_kernel(const float* __restrict__ part, int M, int nblk, double smooth_nr, double smooth_dr,
-                                   double inv_count, double* __restrict__ dice_map, float* __restrict__ coef) {
-  int m = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void dice_reduce_kernel(const float* __restrict__ part, int M, int nblk,
+                                                          double smooth_nr, double smooth_dr, double inv_count,
+                                                          double* __restrict__ dice_map, float* __restrict__ coef) {
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (m >= M) return;
   double I = 0, G = 0, Ps = 0;
-  for (int b = 0; b < nblk; ++b) {
+  for (int b = lane; b < nblk; b += 64) {
     I += part[((long long)m * nblk + b) * 3 + 0];
     G += part[((long long)m * nblk + b) * 3 + 1];
     Ps += part[((long long)m * nblk + b) * 3 + 2];
   }
+  I = wave_sum_d(I);
+  G = wave_sum_d(G);
+  Ps = wave_sum_d(Ps);
+  if (lane) return;
   double num = 2.0 * I + smooth_nr, den = G + Ps + smooth_dr;
   dice_map[m] = 1.0 - num / den;
   coef[2 * m + 0] = (float)(-2.0 / den * inv_count);
@@ -110,40 +145,72 @@ __global__ void dice_reduce_kernel(const float* __restrict__ part, int M, int nb
 }
 
 // per (b, pixel): CE over the N prompt channels + Dice gradient. dmask = w_dice*ddice + w_ce*dce.
-// ce_part[blk] (double) = sum over the block's pixels of sum_n t_n (lse - x_n)
+// ce_part[blk] (double) = sum over the block's pixels of sum_n t_n (lse - x_n). NR > 0: the pixel's N <= NR
+// logits and targets are read once into registers (NR = 0: three strided passes, any N).
+template <int NR>
 __global__ __launch_bounds__(256) void dicece_bwd_kernel(const float* __restrict__ x, const uint8_t* __restrict__ gt,
-                                                         const float* __restrict__ coef, int B, int N, long long HW,
+                                                         const float* __restrict__ coef, int B, int N, int HW,
                                                          float w_dice, float w_ce, float inv_bhw,
                                                          float* __restrict__ dx, double* __restrict__ ce_part) {
-  const long long total = (long long)B * HW;
+  const int total = B * HW;  // host-checked < 2^31
   double ce = 0.0;
-  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    const int b = (int)(e / HW);
-    const long long pix = e % HW;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int b = e / HW, pix = e - b * HW;
     const float* xb = x + (long long)b * N * HW + pix;
     const uint8_t* tb = gt + (long long)b * N * HW + pix;
-    float mx = -INFINITY;
-    for (int n = 0; n < N; ++n) mx = fmaxf(mx, xb[n * HW]);
-    float se = 0.0f, tsum = 0.0f, tx = 0.0f;
-    for (int n = 0; n < N; ++n) {
-      float xv = xb[n * HW];
-      float t = (float)tb[n * HW];
-      se += __expf(xv - mx);
-      tsum += t;
-      tx += t * xv;
-    }
-    const float lse = mx + __logf(se);
-    ce += (double)(lse * tsum - tx);
     float* db = dx + (long long)b * N * HW + pix;
-    for (int n = 0; n < N; ++n) {
-      float xv = xb[n * HW];
-      float t = (float)tb[n * HW];
-      float sm = __expf(xv - lse);
-      float p = 1.0f / (1.0f + __expf(-xv));
-      const float* cf = coef + 2 * (b * N + n);
-      float gd = (cf[0] * t + cf[1]) * p * (1.0f - p);
-      float gc = (sm * tsum - t) * inv_bhw;
-      db[n * HW] = w_dice * gd + w_ce * gc;
+    const float* cfb = coef + 2 * b * N;
+    if constexpr (NR > 0) {
+      float xv[NR], tv[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        xv[n] = n < N ? xb[(long long)n * HW] : -INFINITY;
+        tv[n] = n < N ? (float)tb[(long long)n * HW] : 0.0f;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) mx = fmaxf(mx, xv[n]);
+      float se = 0.0f, tsum = 0.0f, tx = 0.0f;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          se += __expf(xv[n] - mx);
+          tsum += tv[n];
+          tx += tv[n] * xv[n];
+        }
+      }
+      const float lse = mx + __logf(se);
+      ce += (double)(lse * tsum - tx);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          const float sm = __expf(xv[n] - lse);
+          const float p = 1.0f / (1.0f + __expf(-xv[n]));
+          const float gd = (cfb[2 * n] * tv[n] + cfb[2 * n + 1]) * p * (1.0f - p);
+          const float gc = (sm * tsum - tv[n]) * inv_bhw;
+          db[(long long)n * HW] = w_dice * gd + w_ce * gc;
+        }
+      }
+    } else {
+      float mx = -INFINITY;
+      for (int n = 0; n < N; ++n) mx = fmaxf(mx, xb[(long long)n * HW]);
+      float se = 0.0f, tsum = 0.0f, tx = 0.0f;
+      for (int n = 0; n < N; ++n) {
+        const float xv = xb[(long long)n * HW], t = (float)tb[(long long)n * HW];
+        se += __expf(xv - mx);
+        tsum += t;
+        tx += t * xv;
+      }
+      const float lse = mx + __logf(se);
+      ce += (double)(lse * tsum - tx);
+      for (int n = 0; n < N; ++n) {
+        const float xv = xb[(long long)n * HW], t = (float)tb[(long long)n * HW];
+        const float sm = __expf(xv - lse);
+        const float p = 1.0f / (1.0f + __expf(-xv));
+        const float gd = (cfb[2 * n] * t + cfb[2 * n + 1]) * p * (1.0f - p);
+        const float gc = (sm * tsum - t) * inv_bhw;
+        db[(long long)n * HW] = w_dice * gd + w_ce * gc;
+      }
     }
   }
   __shared__ double red[4];
@@ -168,18 +235,29 @@ __global__ void loss_finalize_kernel(const double* __restrict__ dice_map, int M,
 }
 
 // Backward of the composite post-processing operator: dlow[m] = Wy^T dout[m] Wx.
-// Row pass: tmp[m][i][b] = sum_{(j,w) in colcsr[b]} w * dout[m][i][j]
+// Row pass: tmp[m][i][b] = sum_{(j,w) in colcsr[b]} w * dout[m][i][j]; 4 rows of dout per workgroup staged
+// in LDS by coalesced loads (ow <= 1024, host-checked), thread b walks column b's taps once for all 4 rows.
 __global__ __launch_bounds__(256) void pp_bwd_rows_kernel(const float* __restrict__ dout, int oh, int ow, int S,
                                                           const int* __restrict__ cptr, const int* __restrict__ cidx,
                                                           const float* __restrict__ cw, float* __restrict__ tmp) {
-  const int m = blockIdx.y;
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (long long)oh * S) return;
-  const int i = (int)(e / S), b = (int)(e % S);
-  const float* row = dout + ((long long)m * oh + i) * ow;
-  float acc = 0.0f;
-  for (int k = cptr[b]; k < cptr[b + 1]; ++k) acc += cw[k] * row[cidx[k]];
-  tmp[((long long)m * oh + i) * S + b] = acc;
+  __shared__ float rows[4][1024];
+  const int m = blockIdx.y, i0 = blockIdx.x * 4, tid = threadIdx.x;
+  const int nr = min(4, oh - i0);
+  for (int e = tid; e < nr * ow; e += 256) {
+    const int r = e / ow, j = e - r * ow;
+    rows[r][j] = dout[((long long)m * oh + i0 + r) * ow + j];
+  }
+  __syncthreads();
+  for (int b = tid; b < S; b += 256) {
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int k = cptr[b]; k < cptr[b + 1]; ++k) {
+      const int j = cidx[k];
+      const float wv = cw[k];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += wv * rows[r][j];
+    }
+    for (int r = 0; r < nr; ++r) tmp[((long long)m * oh + i0 + r) * S + b] = acc[r];
+  }
 }
 // Column pass: dlow[m][a][b] = sum_{(i,w) in rowcsr[a]} w * tmp[m][i][b]
 __global__ __launch_bounds__(256) void pp_bwd_cols_kernel(const float* __restrict__ tmp, int oh, int S,
@@ -254,9 +332,18 @@ extern "C" int octsam_postproc_fwd(const float* lowres, int32_t M, int32_t S, in
                        crop_h <= mid && crop_w <= mid && nblk > 0,
                    "octsam_postproc_fwd: bad args");
   OCTSAM_CHECK_ARG(!gt || dice_part, "octsam_postproc_fwd: gt needs dice_part");
+  OCTSAM_CHECK_ARG((long long)out_h * out_w < (1 << 24), "octsam_postproc_fwd: output too large (%d x %d)", out_h,
+                   out_w);
   PP pp{S, mid, crop_h, crop_w, out_h, out_w, (float)S / (float)mid, (float)crop_h / (float)out_h,
         (float)crop_w / (float)out_w};
-  hipLaunchKernelGGL(postproc_fwd_kernel, dim3(nblk, M), dim3(256), 0, (hipStream_t)stream, lowres, pp, out, gt,
+  const int ngrp = (out_h + PP_ROWS - 1) / PP_ROWS;
+  OCTSAM_CHECK_ARG(S <= 256 && S % 4 == 0 && ((uintptr_t)lowres & 15) == 0 && (!gt || nblk == ngrp),
+                   "octsam_postproc_fwd: needs S <= 256, S %% 4 == 0, 16-B aligned lowres and nblk == ceil(out_h/4)");
+  // the low-res rows of 4 consecutive output rows must fit the LDS range (PP_LRMAX): originals down to
+  // ~1/12 of the crop
+  OCTSAM_CHECK_ARG((double)PP_ROWS * crop_h / out_h * S / mid + 4.0 <= PP_LRMAX,
+                   "octsam_postproc_fwd: output rows too coarse for the staged low-res range");
+  hipLaunchKernelGGL(postproc_fwd_kernel, dim3(ngrp, M), dim3(256), 0, (hipStream_t)stream, lowres, pp, out, gt,
                      dice_part);
   OCTSAM_LAUNCH_CHECK("octsam_postproc_fwd");
   return 0;
@@ -265,7 +352,7 @@ extern "C" int octsam_postproc_fwd(const float* lowres, int32_t M, int32_t S, in
 extern "C" int octsam_dice_reduce(const float* dice_part, int32_t M, int32_t nblk, double* dice_map, float* coef,
                                   void* stream) {
   OCTSAM_CHECK_ARG(dice_part && dice_map && coef && M > 0 && nblk > 0, "octsam_dice_reduce: bad args");
-  hipLaunchKernelGGL(dice_reduce_kernel, dim3((M + 127) / 128), dim3(128), 0, (hipStream_t)stream, dice_part, M, nblk,
+  hipLaunchKernelGGL(dice_reduce_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, dice_part, M, nblk,
                      1e-5, 1e-5, 1.0 / M, dice_map, coef);
   OCTSAM_LAUNCH_CHECK("octsam_dice_reduce");
   return 0;
@@ -276,8 +363,15 @@ extern "C" int octsam_dicece_bwd(const float* masks, const uint8_t* gt, const fl
                                  void* stream) {
   OCTSAM_CHECK_ARG(masks && gt && coef && dmask && ce_part && B > 0 && N > 0 && HW > 0 && nblk > 0,
                    "octsam_dicece_bwd: bad args");
-  hipLaunchKernelGGL(dicece_bwd_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, masks, gt, coef, B, N, HW, w_dice,
-                     w_ce, (float)(1.0 / ((double)B * HW)), dmask, ce_part);
+  OCTSAM_CHECK_ARG((long long)B * HW < (1LL << 31), "octsam_dicece_bwd: B*HW too large");
+  const float inv = (float)(1.0 / ((double)B * HW));
+  hipStream_t s = (hipStream_t)stream;
+  if (N <= 32)
+    hipLaunchKernelGGL(dicece_bwd_kernel<32>, dim3(nblk), dim3(256), 0, s, masks, gt, coef, B, N, (int)HW, w_dice, w_ce,
+                       inv, dmask, ce_part);
+  else
+    hipLaunchKernelGGL(dicece_bwd_kernel<0>, dim3(nblk), dim3(256), 0, s, masks, gt, coef, B, N, (int)HW, w_dice, w_ce,
+                       inv, dmask, ce_part);
   OCTSAM_LAUNCH_CHECK("octsam_dicece_bwd");
   return 0;
 }
@@ -298,8 +392,9 @@ extern "C" int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int3
   OCTSAM_CHECK_ARG(dout && col_ptr && col_idx && col_w && row_ptr && row_idx && row_w && tmp && dlowres && M > 0,
                    "octsam_postproc_bwd: bad args");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(pp_bwd_rows_kernel, dim3((unsigned)(((long long)out_h * S + 255) / 256), M), dim3(256), 0, s, dout,
-                     out_h, out_w, S, col_ptr, col_idx, col_w, tmp);
+  OCTSAM_CHECK_ARG(out_w <= 1024, "octsam_postproc_bwd: out_w must be <= 1024");
+  hipLaunchKernelGGL(pp_bwd_rows_kernel, dim3((unsigned)((out_h + 3) / 4), M), dim3(256), 0, s, dout, out_h, out_w, S,
+                     col_ptr, col_idx, col_w, tmp);
   OCTSAM_LAUNCH_CHECK("octsam_postproc_bwd");
   hipLaunchKernelGGL(pp_bwd_cols_kernel, dim3((S * S + 255) / 256, M), dim3(256), 0, s, tmp, out_h, S, row_ptr, row_idx,
                      row_w, dlowres);

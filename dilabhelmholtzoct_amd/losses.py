@@ -74,10 +74,11 @@ def pp_tables(S, mid, ch, cw, oh, ow, device):
     return _DEV_TABLES[key]
 
 
-def postproc_forward(low: torch.Tensor, crop, orig, gt_u8=None, nblk: int = 16):
-    """low fp32 [M, 256, 256] -> masks fp32 [M, oh, ow]; with gt also the Dice partials."""
+def postproc_forward(low: torch.Tensor, crop, orig, gt_u8=None):
+    """low fp32 [M, 256, 256] -> masks fp32 [M, oh, ow]; with gt also the Dice partials (one per 4 output rows)."""
     M, S, _ = low.shape
     (ch, cw), (oh, ow) = crop, orig
+    nblk = (oh + 3) // 4
     out = torch.empty(M, oh, ow, device=low.device, dtype=torch.float32)
     part = torch.empty(M, nblk, 3, device=low.device, dtype=torch.float32) if gt_u8 is not None else None
     _lib.call("octsam_postproc_fwd", K.ptr(low), M, S, 1024, ch, cw, oh, ow, K.ptr(out), K.ptr(gt_u8), K.ptr(part),
