@@ -145,3 +145,16 @@ def test_patchify_bf16(cuda):
     kernels.patchify_bf16(px, out)
     ref = px.view(B, 3, 64, 16, 64, 16).permute(0, 2, 4, 1, 3, 5).reshape(B * 4096, 768).to(torch.bfloat16)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("ld,cols,off", [(256, 128, 0), (256, 128, 128), (128, 128, 0), (24, 12, 0)])
+def test_group_sum(cuda, ld, cols, off):
+    """out[g] = sum over the nper prompt blocks of image g (fixed order), strided column window; bf16 out."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(ld + cols + off)
+    G, nper, rows = 3, 5, 4096
+    x = torch.randn(G * nper * rows, ld, generator=g).to(cuda, torch.bfloat16)
+    out = torch.empty(G * rows, cols, device=cuda, dtype=torch.bfloat16)
+    kernels.group_sum(x[:, off:], out, ld_in=ld, cols=cols, groups=G, nper=nper, rows_per=rows)
+    ref = x[:, off:off + cols].float().view(G, nper, rows, cols).sum(1).reshape(G * rows, cols)
+    assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
