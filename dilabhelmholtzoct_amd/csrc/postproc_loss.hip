@@ -220,15 +220,27 @@ __global__ __launch_bounds__(256) void dicece_bwd_kernel(const float* __restrict
   if (threadIdx.x == 0) ce_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// loss[0] = mean dice, loss[1] = ce, loss[2] = w_dice*dice + w_ce*ce
-__global__ void loss_finalize_kernel(const double* __restrict__ dice_map, int M, const double* __restrict__ ce_part,
-                                     int nblk, double inv_bhw, double w_dice, double w_ce, double* __restrict__ loss) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// loss[0] = mean dice, loss[1] = ce, loss[2] = w_dice*dice + w_ce*ce; one 256-thread block, strided sums then
+// a fixed reduction tree (deterministic)
+__global__ __launch_bounds__(256) void loss_finalize_kernel(const double* __restrict__ dice_map, int M,
+                                                            const double* __restrict__ ce_part, int nblk,
+                                                            double inv_bhw, double w_dice, double w_ce,
+                                                            double* __restrict__ loss) {
+  __shared__ double red[2][4];
   double d = 0.0, c = 0.0;
-  for (int m = 0; m < M; ++m) d += dice_map[m];
-  for (int b = 0; b < nblk; ++b) c += ce_part[b];
-  d /= M;
-  c *= inv_bhw;
+  for (int m = threadIdx.x; m < M; m += 256) d += dice_map[m];
+  for (int b = threadIdx.x; b < nblk; b += 256) c += ce_part[b];
+  d = wave_sum_d(d);
+  c = wave_sum_d(c);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wave] = d;
+    red[1][wave] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  d = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / M;
+  c = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) * inv_bhw;
   loss[0] = d;
   loss[1] = c;
   loss[2] = w_dice * d + w_ce * c;
@@ -379,7 +391,7 @@ extern "C" int octsam_dicece_bwd(const float* masks, const uint8_t* gt, const fl
 extern "C" int octsam_loss_finalize(const double* dice_map, int32_t M, const double* ce_part, int32_t nblk, int32_t B,
                                     int64_t HW, double w_dice, double w_ce, double* loss, void* stream) {
   OCTSAM_CHECK_ARG(dice_map && ce_part && loss && M > 0 && nblk > 0, "octsam_loss_finalize: bad args");
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dice_map, M, ce_part, nblk,
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, dice_map, M, ce_part, nblk,
                      1.0 / ((double)B * HW), w_dice, w_ce, loss);
   OCTSAM_LAUNCH_CHECK("octsam_loss_finalize");
   return 0;

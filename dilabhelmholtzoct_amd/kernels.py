@@ -102,6 +102,8 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     rows = mean.numel()
     if D <= 64:
         nblocks = max(nblocks, 4096)
+    elif rows >= 65536:
+        nblocks = max(nblocks, 1280)  # image-side rows: 5 waves per SIMD (the kernel's occupancy) in flight
     nblocks = max(1, min(nblocks, (rows + 3) // 4))
     part = torch.empty((2, nblocks, D), device=dy.device, dtype=torch.float32)
     _lib.call("octsam_layernorm_bwd", ptr(dy), int(dy.dtype == torch.float32), ptr(x),
