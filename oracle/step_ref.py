@@ -33,10 +33,14 @@ def synthetic_state_dict(base_model: str, seed: int = 0):
 
 class CpuReferenceStep:
     def __init__(self, base_model="facebook/sam-vit-base", topological=False, seed=0, lr=1e-3, weight_decay=0.0,
-                 topo_mode="first", state_dict=None):
+                 topo_mode="first", state_dict=None, device="cpu"):
+        """device: where the fp32 SamModel runs (CPU for the bench baseline; a GPU only to speed up the
+        val-Dice parity test). Post-processing and losses always run on the CPU in fp32/f64."""
         from transformers import SamModel
         self.model = SamModel(hf_config(base_model)).float()
         self.model.load_state_dict(state_dict if state_dict is not None else synthetic_state_dict(base_model, seed))
+        self.device = torch.device(device)
+        self.model.to(self.device)
         for name, p in self.model.named_parameters():  # training_utils.py:277-279
             if name.startswith("vision_encoder") or name.startswith("prompt_encoder"):
                 p.requires_grad_(False)
@@ -44,19 +48,25 @@ class CpuReferenceStep:
         self.topological = topological
         self.topo_mode = topo_mode
 
-    def forward_loss(self, batch):
-        inputs = {"pixel_values": batch["pixel_values"].float()}
+    def predict(self, batch):
+        """Post-processed fp32 logits [B, N, H, W] on the CPU (training_utils.py:56-58 / :121-125)."""
+        dev = self.device
+        inputs = {"pixel_values": batch["pixel_values"].float().to(dev)}
         if "input_boxes" in batch:
-            inputs["input_boxes"] = batch["input_boxes"]
+            inputs["input_boxes"] = batch["input_boxes"].to(dev)
         if "input_points" in batch:
-            inputs["input_points"] = batch["input_points"]
-        gt = batch["gt_u8"].double()
+            inputs["input_points"] = batch["input_points"].to(dev)
         out = self.model(**inputs, multimask_output=False)
-        masks = F.interpolate(out.pred_masks.squeeze(2), (1024, 1024), mode="bilinear", align_corners=False)
+        masks = F.interpolate(out.pred_masks.squeeze(2).cpu(), (1024, 1024), mode="bilinear",
+                              align_corners=False)
         rh, rw = (int(v) for v in batch["reshaped_input_sizes"][0])
         oh, ow = (int(v) for v in batch["original_sizes"][0])
         masks = masks[..., :rh, :rw]
-        masks = F.interpolate(masks, (oh, ow), mode="bilinear", align_corners=False)
+        return F.interpolate(masks, (oh, ow), mode="bilinear", align_corners=False)
+
+    def forward_loss(self, batch):
+        gt = batch["gt_u8"].cpu().double()
+        masks = self.predict(batch)
         loss = dicece_ref(masks, gt)
         topo = torch.zeros((), dtype=torch.float64)
         if self.topological:
