@@ -67,6 +67,9 @@ _SIGNATURES = {
     "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "octsam_patchify_bf16": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "octsam_sam_preprocess": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32,
+                                        c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32,
+                                        c_int32, c_void_p]),
     "octsam_dec_tok_attn_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                           c_void_p]),
     "octsam_dec_tok_attn_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,

@@ -167,6 +167,21 @@ def process_batch(processor, batch, prompt_type: str = "bboxes"):
     return out
 
 
+def process_batch_device(processor, batch, prompt_type: str = "bboxes"):
+    """process_batch with the image path on the GPU (preprocess.DeviceProcessor: Pillow-exact resize +
+    normalise + pad as one HIP kernel, bit-identical to SamProcessor's pixel_values); prompts, sizes and gt
+    stay host tensors like process_batch's, pixel_values is already on the processor's device."""
+    image, prompt, gt_masks, mask_values = batch
+    images = image.to(processor.device, non_blocking=True)
+    if prompt_type == "points":
+        out = processor(images, input_points=prompt)
+    else:
+        out = processor(images, input_boxes=prompt)
+    out["gt_u8"] = gt_masks.round().clamp(0, 1).to(torch.uint8)
+    out["mask_values"] = mask_values
+    return out
+
+
 def pad_prompts(batch: dict, n_target: int) -> dict:
     """Pad the prompt dimension to n_target with the collate's zero padding (global-N padding across
     data-parallel ranks, so every rank sees the batch the single-process collate would build)."""

@@ -398,7 +398,11 @@ def _load_split(config: dict, split: str):
 
 def _batch_for(items, processor, prompt, n_target, device):
     from . import data
-    b = data.process_batch(processor, data.custom_collate(items), prompt)
+    from .preprocess import DeviceProcessor
+    if isinstance(processor, DeviceProcessor):
+        b = data.process_batch_device(processor, data.custom_collate(items), prompt)
+    else:
+        b = data.process_batch(processor, data.custom_collate(items), prompt)
     b = data.pad_prompts(b, n_target)
     return data.to_device_batch(b, device)
 
@@ -425,7 +429,11 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     rank = dist.get_rank(pg) if pg is not None else 0
     device = device or torch.device("cuda", torch.cuda.current_device())
     model = SamModel.from_pretrained(base_model, seed=config.get("seed", 0)).to(device)
-    processor = data.make_processor()
+    if device.type == "cuda" and config.get("gpu_processor", True):  # image path as a HIP kernel (§8(f)1)
+        from .preprocess import DeviceProcessor
+        processor = DeviceProcessor(device)
+    else:
+        processor = data.make_processor()
     train_data = train_data if train_data is not None else _load_split(config, "train")
     valid_data = valid_data if valid_data is not None else _load_split(config, "test")
     prompt = config.get("prompt_type", "bboxes")

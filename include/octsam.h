@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 3
+#define OCTSAM_ABI_VERSION 4
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -163,6 +163,18 @@ int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 /* Patch-embedding operand: pixel_values fp32 [B, 3, 1024, 1024] -> bf16 [B*4096, 768], row = (b, py, px),
  * k = (c, ky, kx) (= Conv2d(3, D, 16, 16) weight.reshape(D, 768) order); replaces the gathered a_mode 2. */
 int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream);
+
+/* ---------------------------------------------------------------- image processor (A3)
+ * SamProcessor image path (hf:image_processing_pil_sam.py:227-263 with Pillow's BILINEAR 8-bpc
+ * ImagingResample): uint8 HWC RGB images [B, H, W, 3] (image b at images + b*img_stride) -> fp32 planar
+ * [B, 3, out_h, out_w]: two-pass fixed-point resize to rh x rw, then lut[c*256 + v] (= rescale 1/255 and
+ * (x - mean_c) / std_c in the processor's float arithmetic), zero padding outside rh x rw.
+ * xtab [rw, 2 + kx] / ytab [rh, 2 + ky] int32 rows = (first source index, taps, kx (ky) weights of 22
+ * fractional bits) as built by dilabhelmholtzoct_amd/preprocess.resample_table. Bit-exact with Pillow.
+ * Requires 1 <= kx, ky <= 16, out_w % 4 == 0, out 16-B aligned, ky*W*3 <= 65536. */
+int octsam_sam_preprocess(const uint8_t* images, int32_t B, int32_t H, int32_t W, int64_t img_stride,
+                          const int32_t* xtab, int32_t kx, const int32_t* ytab, int32_t ky, int32_t rh,
+                          int32_t rw, const float* lut, float* out, int32_t out_h, int32_t out_w, void* stream);
 
 /* ---------------------------------------------------------------- mask decoder attention cores
  * SamAttention core softmax(q k^T / sqrt(dh)) v (hf:modeling_sam.py:231-270) for the three shapes of
