@@ -67,6 +67,10 @@ _SIGNATURES = {
     "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "octsam_patchify_bf16": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "octsam_cc_label": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
+                                  c_void_p]),
+    "octsam_cc_assign": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int32, c_void_p]),
     "octsam_sam_preprocess": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32,
                                         c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32,
                                         c_int32, c_void_p]),

@@ -1,0 +1,145 @@
+"""Prompt and gt generation on the GPU: the label-map half of
+``SAMDataset.__getitem__`` + ``custom_collate`` (ref:octsam/models/training_utils.py:381-458).
+
+The reference, per sample: for v in np.unique(label), for each 8-connected component of (label == v) in
+scipy.ndimage.label order: the bbox of its pixels jittered by four ``np.random.randint(-10, 10)`` draws
+(x_min, x_max, y_min, y_max; clamped to [0, W] / [0, H]) or one ``random.randrange(0, n_pixels)`` pixel in
+``np.where`` (raster) order, the float64 component indicator as gt, and v as the mask value; the collate
+zero-pads to the batch's max component count.
+
+Here the components, their rank (the reference order = sort by (value, first raster pixel)), per-component
+bboxes / pixel counts and the uint8 gt [B, N, H, W] come from csrc/components.hip; only the per-image root
+keys (a few dozen ints), the bbox table and the counts cross to the host, where the reference's RNG draws
+are replayed in its order (seed hooks per sample as SAMDataset applies them).
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+
+MAX_COMPONENTS = 1024
+
+
+class DeviceComponents:
+    """Connected components + component statistics of uint8 label maps on one device."""
+
+    def __init__(self, device, max_components: int = MAX_COMPONENTS):
+        self.device = torch.device(device)
+        self.maxc = int(max_components)
+        if not 1 <= self.maxc <= MAX_COMPONENTS:
+            raise ValueError(f"max_components must be in [1, {MAX_COMPONENTS}]")
+
+    def __call__(self, labels: torch.Tensor, n_target: int | None = None, want_gt: bool = True):
+        """labels uint8 [B, H, W] on the device. Returns dict:
+        comp int32 [B, H, W] (component rank per pixel, device), ncomp list[int], values list[np.uint8 [n]],
+        stats list[np.int64 [n, 5]] (xmin, xmax, ymin, ymax, pixels), gt uint8 [B, N, H, W] (device,
+        N = max(ncomp, n_target), zero-padded components) when want_gt."""
+        if labels.dtype != torch.uint8 or labels.dim() != 3:
+            raise ValueError(f"labels must be uint8 [B, H, W], got {labels.dtype} {tuple(labels.shape)}")
+        if labels.device != self.device:
+            raise ValueError(f"labels on {labels.device}, components on {self.device}")
+        labels = labels.contiguous()
+        B, H, W = labels.shape
+        dev = self.device
+        parent = torch.empty(B * H * W, device=dev, dtype=torch.int32)
+        roots = torch.empty(B, self.maxc, device=dev, dtype=torch.int32)
+        nroots = torch.empty(B, device=dev, dtype=torch.int32)
+        _lib.call("octsam_cc_label", _lib.ptr(labels), B, H, W, _lib.ptr(parent), _lib.ptr(roots), self.maxc,
+                  _lib.ptr(nroots))
+        counts = nroots.cpu().numpy()
+        if int(counts.max()) > self.maxc:
+            raise ValueError(f"a label map has {int(counts.max())} components (> {self.maxc})")
+        keys = roots.cpu().numpy()
+        sorted_roots = np.zeros((B, self.maxc), dtype=np.int32)
+        values = []
+        for b in range(B):
+            # keys as unsigned 32-bit: (value, first pixel) = the reference's order
+            k = np.sort(keys[b, :counts[b]].astype(np.int64) & 0xFFFFFFFF)
+            sorted_roots[b, :len(k)] = (k & 0xFFFFFF).astype(np.int32)
+            values.append((k >> 24).astype(np.uint8))
+        ncomp = [int(c) for c in counts]
+        N = max(max(ncomp), n_target or 0)
+        comp = torch.empty(B, H, W, device=dev, dtype=torch.int32)
+        stats = torch.empty(B, self.maxc, 5, device=dev, dtype=torch.int32)
+        gt = None
+        if want_gt:
+            if (H * W) % 16:
+                raise ValueError("gt output needs H*W % 16 == 0")
+            gt = torch.empty(B, N, H, W, device=dev, dtype=torch.uint8)
+        # (named: a temporary's block would return to the allocator before the launch reads it)
+        roots_d = torch.from_numpy(sorted_roots).to(dev)
+        ncomp_d = torch.from_numpy(counts.astype(np.int32)).to(dev)
+        _lib.call("octsam_cc_assign", _lib.ptr(parent), B, H, W, _lib.ptr(roots_d), self.maxc, _lib.ptr(ncomp_d),
+                  _lib.ptr(comp), _lib.ptr(stats), _lib.ptr(gt), N)
+        st = stats.cpu().numpy().astype(np.int64)
+        return {"comp": comp, "ncomp": ncomp, "values": values, "stats": [st[b, :ncomp[b]] for b in range(B)],
+                "gt": gt, "N": N}
+
+
+def bbox_prompts(stats: np.ndarray, H: int, W: int) -> list:
+    """get_bboxes_and_gt_masks (training_utils.py:389-415) for one sample, components in order: the
+    jittered [x_min, y_min, x_max, y_max] with the reference's draw order and clamps."""
+    out = []
+    for xmin, xmax, ymin, ymax, _ in stats:
+        x_min = max(0, np.int64(xmin) + np.random.randint(-10, 10))
+        x_max = min(W, np.int64(xmax) + np.random.randint(-10, 10))
+        y_min = max(0, np.int64(ymin) + np.random.randint(-10, 10))
+        y_max = min(H, np.int64(ymax) + np.random.randint(-10, 10))
+        out.append([x_min, y_min, x_max, y_max])
+    return out
+
+
+def point_prompts(stats: np.ndarray, comp_b: np.ndarray) -> list:
+    """get_points_and_gt_masks (training_utils.py:417-434) for one sample: random.randrange over the
+    component's pixels in raster order; comp_b = that sample's rank map [H, W] (host)."""
+    W = comp_b.shape[1]
+    flat = comp_b.reshape(-1)
+    out = []
+    for n, row in enumerate(stats):
+        k = random.randrange(0, int(row[4]))
+        idx = int(np.flatnonzero(flat == n)[k])
+        out.append([[np.int64(idx % W), np.int64(idx // W)]])
+    return out
+
+
+def collate_device(images: np.ndarray | torch.Tensor, labels: np.ndarray | torch.Tensor, prompt_type: str,
+                   device, seed_hooks=None, n_target: int | None = None, processor=None) -> dict:
+    """SAMDataset items + custom_collate + SamProcessor for a batch with the label and image work on the
+    device. images uint8 [B, H, W, 3], labels uint8 [B, H, W]; seed_hooks: optional list of B callables
+    run before each sample's draws (SAMDataset's per-item seeding). Returns the process_batch dict
+    (pixel_values and gt_u8 on the device; prompts float64, mask_values uint8 on the host)."""
+    from .preprocess import DeviceProcessor
+    dev = torch.device(device)
+    labels = torch.as_tensor(labels).to(dev)
+    images = torch.as_tensor(images)
+    B, H, W = labels.shape
+    cc = DeviceComponents(dev)(labels, n_target=n_target)
+    comp_h = cc["comp"].cpu().numpy() if prompt_type == "points" else None
+    prompts = []
+    for b in range(B):
+        if seed_hooks is not None:
+            seed_hooks[b]()
+        if prompt_type == "points":
+            prompts.append(point_prompts(cc["stats"][b], comp_h[b]))
+        else:
+            prompts.append(bbox_prompts(cc["stats"][b], H, W))
+    N = cc["N"]
+    shape = (B, N, 1, 2) if prompt_type == "points" else (B, N, 4)
+    prompt = np.zeros(shape, dtype=np.int64)
+    mask_values = torch.zeros(B, N, dtype=torch.uint8)
+    for b in range(B):
+        n = cc["ncomp"][b]
+        if n:
+            prompt[b, :n] = np.asarray(prompts[b], dtype=np.int64).reshape((n,) + shape[2:])
+            mask_values[b, :n] = torch.from_numpy(cc["values"][b])
+    proc = processor if processor is not None else DeviceProcessor(dev)
+    key = "input_points" if prompt_type == "points" else "input_boxes"
+    out = proc(images.to(dev), **{key: prompt})
+    out["gt_u8"] = cc["gt"]
+    out["mask_values"] = mask_values
+    out["prompt_raw"] = torch.from_numpy(prompt)
+    return out

@@ -126,8 +126,9 @@ def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor,
         raise ValueError("vit_attention expects bf16 qkv/out")
     if qkv.numel() != nseq * side * side * 3 * heads * 64:
         raise ValueError("qkv shape does not match nseq/side/heads")
-    _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rel_pos_h.float().contiguous()),
-              ptr(rel_pos_w.float().contiguous()), nseq, side, heads, 64)
+    rh = rel_pos_h.float().contiguous()  # (named, so a converted copy outlives the launch)
+    rw = rel_pos_w.float().contiguous()
+    _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rh), ptr(rw), nseq, side, heads, 64)
     return out
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 4
+#define OCTSAM_ABI_VERSION 5
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -163,6 +163,22 @@ int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 /* Patch-embedding operand: pixel_values fp32 [B, 3, 1024, 1024] -> bf16 [B*4096, 768], row = (b, py, px),
  * k = (c, ky, kx) (= Conv2d(3, D, 16, 16) weight.reshape(D, 768) order); replaces the gathered a_mode 2. */
 int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream);
+
+/* ---------------------------------------------------------------- label components (A2)
+ * SAMDataset._components (ref:octsam/models/training_utils.py:389-434: np.unique values, scipy.ndimage.label
+ * with the 3x3 structure) on the GPU. octsam_cc_label: labels uint8 [B, H, W] (H*W < 2^24) -> parent int32
+ * [B*H*W] (each pixel's root = first raster pixel of its 8-connected equal-value component) and, per image,
+ * the unordered root keys (value << 24 | root index) in roots [B, max_roots] with their count in nroots [B]
+ * (counts beyond max_roots are counted, not stored). The host sorts the keys: that is the reference's
+ * component order. octsam_cc_assign: sorted_roots [B, maxc] root indices, ncomp [B] (<= maxc <= 1024) ->
+ * comp int32 [B, H, W] = component rank of every pixel, stats int32 [B, maxc, 5] = (xmin, xmax, ymin,
+ * ymax, pixel count); if gt != NULL also gt uint8 [B, N, H, W] = (comp == n) (H*W % 16 == 0, 16-B
+ * aligned gt and comp). */
+int octsam_cc_label(const uint8_t* labels, int32_t B, int32_t H, int32_t W, int32_t* parent, int32_t* roots,
+                    int32_t max_roots, int32_t* nroots, void* stream);
+int octsam_cc_assign(const int32_t* parent, int32_t B, int32_t H, int32_t W, const int32_t* sorted_roots,
+                     int32_t maxc, const int32_t* ncomp, int32_t* comp, int32_t* stats, uint8_t* gt, int32_t N,
+                     void* stream);
 
 /* ---------------------------------------------------------------- image processor (A3)
  * SamProcessor image path (hf:image_processing_pil_sam.py:227-263 with Pillow's BILINEAR 8-bpc
