@@ -38,6 +38,11 @@ class DeviceComponents:
         comp int32 [B, H, W] (component rank per pixel, device), ncomp list[int], values list[np.uint8 [n]],
         stats list[np.int64 [n, 5]] (xmin, xmax, ymin, ymax, pixels), gt uint8 [B, N, H, W] (device,
         N = max(ncomp, n_target), zero-padded components) when want_gt."""
+        return self.assign(self.label(labels), n_target, want_gt)
+
+    def label(self, labels: torch.Tensor) -> dict:
+        """Phase 1: components and their reference order; ``ncomp`` is known after this (the data-parallel
+        loop takes the global max of it before phase 2 sizes the gt)."""
         if labels.dtype != torch.uint8 or labels.dim() != 3:
             raise ValueError(f"labels must be uint8 [B, H, W], got {labels.dtype} {tuple(labels.shape)}")
         if labels.device != self.device:
@@ -61,7 +66,14 @@ class DeviceComponents:
             k = np.sort(keys[b, :counts[b]].astype(np.int64) & 0xFFFFFFFF)
             sorted_roots[b, :len(k)] = (k & 0xFFFFFF).astype(np.int32)
             values.append((k >> 24).astype(np.uint8))
-        ncomp = [int(c) for c in counts]
+        return {"shape": (B, H, W), "parent": parent, "sorted_roots": sorted_roots, "counts": counts,
+                "values": values, "ncomp": [int(c) for c in counts]}
+
+    def assign(self, st: dict, n_target: int | None = None, want_gt: bool = True) -> dict:
+        """Phase 2: ranks, statistics and (optionally) the gt masks padded to max(ncomp, n_target)."""
+        B, H, W = st["shape"]
+        dev = self.device
+        ncomp = st["ncomp"]
         N = max(max(ncomp), n_target or 0)
         comp = torch.empty(B, H, W, device=dev, dtype=torch.int32)
         stats = torch.empty(B, self.maxc, 5, device=dev, dtype=torch.int32)
@@ -69,15 +81,16 @@ class DeviceComponents:
         if want_gt:
             if (H * W) % 16:
                 raise ValueError("gt output needs H*W % 16 == 0")
-            gt = torch.empty(B, N, H, W, device=dev, dtype=torch.uint8)
+            gt = torch.empty(B, max(N, 1), H, W, device=dev, dtype=torch.uint8)
         # (named: a temporary's block would return to the allocator before the launch reads it)
-        roots_d = torch.from_numpy(sorted_roots).to(dev)
-        ncomp_d = torch.from_numpy(counts.astype(np.int32)).to(dev)
-        _lib.call("octsam_cc_assign", _lib.ptr(parent), B, H, W, _lib.ptr(roots_d), self.maxc, _lib.ptr(ncomp_d),
-                  _lib.ptr(comp), _lib.ptr(stats), _lib.ptr(gt), N)
-        st = stats.cpu().numpy().astype(np.int64)
-        return {"comp": comp, "ncomp": ncomp, "values": values, "stats": [st[b, :ncomp[b]] for b in range(B)],
-                "gt": gt, "N": N}
+        roots_d = torch.from_numpy(st["sorted_roots"]).to(dev)
+        ncomp_d = torch.from_numpy(st["counts"].astype(np.int32)).to(dev)
+        _lib.call("octsam_cc_assign", _lib.ptr(st["parent"]), B, H, W, _lib.ptr(roots_d), self.maxc,
+                  _lib.ptr(ncomp_d), _lib.ptr(comp), _lib.ptr(stats), _lib.ptr(gt), max(N, 1))
+        s = stats.cpu().numpy().astype(np.int64)
+        return {"comp": comp, "ncomp": ncomp, "values": st["values"],
+                "stats": [s[b, :ncomp[b]] for b in range(B)], "gt": gt[:, :N] if gt is not None else None,
+                "N": N}
 
 
 def bbox_prompts(stats: np.ndarray, H: int, W: int) -> list:
@@ -106,18 +119,21 @@ def point_prompts(stats: np.ndarray, comp_b: np.ndarray) -> list:
     return out
 
 
-def collate_device(images: np.ndarray | torch.Tensor, labels: np.ndarray | torch.Tensor, prompt_type: str,
-                   device, seed_hooks=None, n_target: int | None = None, processor=None) -> dict:
-    """SAMDataset items + custom_collate + SamProcessor for a batch with the label and image work on the
-    device. images uint8 [B, H, W, 3], labels uint8 [B, H, W]; seed_hooks: optional list of B callables
-    run before each sample's draws (SAMDataset's per-item seeding). Returns the process_batch dict
-    (pixel_values and gt_u8 on the device; prompts float64, mask_values uint8 on the host)."""
-    from .preprocess import DeviceProcessor
+def collate_device_begin(images, labels, prompt_type: str, device, seed_hooks=None) -> dict:
+    """Phase 1 of collate_device: upload, components; the state's ``ncomp`` sizes the (global) batch N."""
     dev = torch.device(device)
     labels = torch.as_tensor(labels).to(dev)
-    images = torch.as_tensor(images)
-    B, H, W = labels.shape
-    cc = DeviceComponents(dev)(labels, n_target=n_target)
+    dc = DeviceComponents(dev)
+    return {"dc": dc, "cc": dc.label(labels), "images": torch.as_tensor(images), "prompt_type": prompt_type,
+            "seed_hooks": seed_hooks, "device": dev}
+
+
+def collate_device_end(state: dict, n_target: int | None = None, processor=None) -> dict:
+    """Phase 2: ranks / statistics / gt, the reference's RNG draws per sample, image processing."""
+    from .preprocess import DeviceProcessor
+    dev, prompt_type, seed_hooks = state["device"], state["prompt_type"], state["seed_hooks"]
+    cc = state["dc"].assign(state["cc"], n_target=n_target)
+    B, H, W = state["cc"]["shape"]
     comp_h = cc["comp"].cpu().numpy() if prompt_type == "points" else None
     prompts = []
     for b in range(B):
@@ -138,8 +154,18 @@ def collate_device(images: np.ndarray | torch.Tensor, labels: np.ndarray | torch
             mask_values[b, :n] = torch.from_numpy(cc["values"][b])
     proc = processor if processor is not None else DeviceProcessor(dev)
     key = "input_points" if prompt_type == "points" else "input_boxes"
-    out = proc(images.to(dev), **{key: prompt})
+    out = proc(state["images"].to(dev), **{key: prompt})
     out["gt_u8"] = cc["gt"]
     out["mask_values"] = mask_values
     out["prompt_raw"] = torch.from_numpy(prompt)
     return out
+
+
+def collate_device(images: np.ndarray | torch.Tensor, labels: np.ndarray | torch.Tensor, prompt_type: str,
+                   device, seed_hooks=None, n_target: int | None = None, processor=None) -> dict:
+    """SAMDataset items + custom_collate + SamProcessor for a batch with the label and image work on the
+    device. images uint8 [B, H, W, 3], labels uint8 [B, H, W]; seed_hooks: optional list of B callables
+    run before each sample's draws (SAMDataset's per-item seeding). Returns the process_batch dict
+    (pixel_values and gt_u8 on the device; prompts float64, mask_values uint8 on the host)."""
+    st = collate_device_begin(images, labels, prompt_type, device, seed_hooks)
+    return collate_device_end(st, n_target, processor)

@@ -16,6 +16,8 @@ import math
 import os
 import time
 
+import numpy as np
+
 import torch
 
 from . import kernels as K
@@ -407,6 +409,41 @@ def _batch_for(items, processor, prompt, n_target, device):
     return data.to_device_batch(b, device)
 
 
+def _prep(ds, idx, prompt, device, device_data):
+    """Phase 1 of a batch: the reference's host items (SAMDataset, scipy components), or — with the HIP data
+    path — device components (components.collate_device_begin, with SAMDataset's per-item seeding replayed).
+    Returns (kind, state, local N)."""
+    from . import data
+    if device_data and idx:
+        from .components import collate_device_begin
+        if ds.config.get("pseudocolor") is not None:
+            raise NotImplementedError("cv2 pseudocolor maps are not available offline")
+        its = [ds.dataset[i] for i in idx]
+        imgs = np.stack([np.array(it["image"]) for it in its])
+        if imgs.ndim == 3:  # grayscale scans: the processor's convert_rgb replicates the channel
+            imgs = np.repeat(imgs[..., None], 3, -1)
+        labs = np.stack([np.array(it["label"]) for it in its]).astype(np.uint8)
+        hooks = None
+        if ds.epoch_seed is not None:
+            hooks = [(lambda i=i: data.seed_sample(ds.epoch, i, ds.epoch_seed)) for i in idx]
+        st = collate_device_begin(imgs, labs, prompt, device, hooks)
+        return "dev", st, max(st["cc"]["ncomp"])
+    items = [ds[i] for i in idx]
+    return "host", items, _n_prompts(items)
+
+
+def _finish(prep, processor, prompt, n_target, device):
+    """Phase 2: the device batch of _prep, padded to the global N."""
+    kind, state, _ = prep
+    if kind == "dev":
+        from .components import collate_device_end
+        from .preprocess import DeviceProcessor
+        b = collate_device_end(state, n_target, processor if isinstance(processor, DeviceProcessor) else None)
+        b.pop("prompt_raw")
+        return b
+    return _batch_for(state, processor, prompt, n_target, device)
+
+
 def _n_prompts(items):
     return max((len(it[3]) for it in items), default=0)
 
@@ -434,6 +471,8 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
         processor = DeviceProcessor(device)
     else:
         processor = data.make_processor()
+    # components / prompts / gt on the GPU too (§8(f)1), with the HIP image processor
+    device_data = device.type == "cuda" and config.get("gpu_processor", True) and config.get("gpu_components", True)
     train_data = train_data if train_data is not None else _load_split(config, "train")
     valid_data = valid_data if valid_data is not None else _load_split(config, "test")
     prompt = config.get("prompt_type", "bboxes")
@@ -454,10 +493,10 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
                 continue
             n_glob = len(tds) - bi * bs * world if bi == len(batches) - 1 else bs * world
             n_glob = min(n_glob, bs * world)
-            items = [tds[i] for i in idx]
-            N = _collective_max(_n_prompts(items), pg)
+            prep = _prep(tds, idx, prompt, device, device_data)
+            N = _collective_max(prep[2], pg)
             if idx:
-                batch = _batch_for(items, processor, prompt, N, device)
+                batch = _finish(prep, processor, prompt, N, device)
                 crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
                 orig = tuple(int(v) for v in batch["original_sizes"][0])
                 loss = step.forward_backward(batch["pixel_values"], batch["gt_u8"],
@@ -472,7 +511,7 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
             epoch_loss += float(_collective_sum(lv.reshape(1), pg)[0]) / n_glob  # the .item() of :69
         step.flush()
         epoch_loss /= len(batches)
-        vloss = validate_model(step, vds, processor, bs, config, world, rank, pg, device)
+        vloss = validate_model(step, vds, processor, bs, config, world, rank, pg, device, device_data)
         hist["train_loss"].append(epoch_loss)
         hist["valid_loss"].append(vloss)
         if rank == 0:
@@ -484,7 +523,7 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
         torch.save(model.state_dict(), ckpt)  # training_utils.py:77 (HF state-dict keys)
     hist["checkpoint"] = ckpt
     if config.get("evaluate", True):
-        conf = evaluate_confusion(model, vds, processor, bs, prompt, world, rank, pg, device)
+        conf = evaluate_confusion(model, vds, processor, bs, prompt, world, rank, pg, device, device_data)
         hist["dice"] = class_dice(conf)
         hist["mean_dice"] = mean_dice(conf)
         if rank == 0:
@@ -493,7 +532,8 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
 
 
 @torch.no_grad()
-def validate_model(step: FusedTrainStep, vds, processor, bs, config, world=1, rank=0, pg=None, device=None):
+def validate_model(step: FusedTrainStep, vds, processor, bs, config, world=1, rank=0, pg=None, device=None,
+                   device_data=False):
     """ref:training_utils.py:351-379, including its double accumulation: every batch adds the DiceCE loss
     and then DiceCE (+ topo) again, divided by len(valid_dl)."""
     prompt = config.get("prompt_type", "bboxes")
@@ -501,11 +541,11 @@ def validate_model(step: FusedTrainStep, vds, processor, bs, config, world=1, ra
     total = 0.0
     for bi, idx in enumerate(batches):
         n_glob = min(bs * world, len(vds) - bi * bs * world)
-        items = [vds[i] for i in idx]
-        N = _collective_max(_n_prompts(items), pg)
+        prep = _prep(vds, idx, prompt, device, device_data)
+        N = _collective_max(prep[2], pg)
         lv = torch.zeros((), dtype=torch.float64)
         if idx:
-            batch = _batch_for(items, processor, prompt, N, device)
+            batch = _finish(prep, processor, prompt, N, device)
             crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
             orig = tuple(int(v) for v in batch["original_sizes"][0])
             loss = step.forward_backward(batch["pixel_values"], batch["gt_u8"], input_boxes=batch.get("input_boxes"),
@@ -518,15 +558,16 @@ def validate_model(step: FusedTrainStep, vds, processor, bs, config, world=1, ra
 
 
 @torch.no_grad()
-def evaluate_confusion(model, vds, processor, bs, prompt, world=1, rank=0, pg=None, device=None):
+def evaluate_confusion(model, vds, processor, bs, prompt, world=1, rank=0, pg=None, device=None,
+                       device_data=False):
     """Pooled per-class (tp, fp, fn) over the validation set (evaluate_metrics, training_utils.py:113-156),
     summed over ranks."""
     conf = torch.zeros(14, 3, dtype=torch.int64)
     for idx in global_batches(len(vds), bs, world, rank):
         if not idx:
             continue
-        items = [vds[i] for i in idx]
-        batch = _batch_for(items, processor, prompt, _n_prompts(items), device)
+        prep = _prep(vds, idx, prompt, device, device_data)
+        batch = _finish(prep, processor, prompt, prep[2], device)
         conf += class_confusion(predict_masks(model, batch), batch["gt_u8"], batch["mask_values"])
     return _collective_sum(conf, pg)
 
