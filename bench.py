@@ -23,6 +23,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "train imgs/sec (1024² OCT, vit-base, top-loss on) + val Dice; 1→8 GPUs"
@@ -48,6 +49,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle step (rank 0, N=1)")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--val", type=int, default=8, help="val images for the Dice readout (0 = skip)")
+    p.add_argument("--data-path", type=int, default=1,
+                   help="time building one batch on the host (reference data path) vs the HIP data path")
     p.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
     p.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
     p.add_argument("--roof-steps", type=int, default=2, help="eager steps timed per GEMM launch for the roofline")
@@ -121,6 +124,47 @@ def make_batch(args, rank, device, processor):
     sd = data.SAMDataset(ds, {"prompt_type": args.prompt}, epoch_seed=rank)
     batch = data.custom_collate([sd[i] for i in range(len(sd))])
     return data.process_batch(processor, batch, args.prompt)
+
+
+def time_data_path(args, device, processor, reps=3):
+    """Outside the timed step: one batch (B images, prompts, gt, pixel_values) built by the reference's host
+    data path (SAMDataset with scipy components + custom_collate + SamProcessor, then the H2D copy) vs the
+    HIP data path (uint8 images / label maps uploaded, components + prompts + gt + processor on the GPU)."""
+    import random
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.components import collate_device
+    from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
+    ds = data.synthetic_oct(seed=77, n=args.batch)
+    imgs = np.stack([np.array(ds[i]["image"]) for i in range(args.batch)])
+    labs = np.stack([np.array(ds[i]["label"]) for i in range(args.batch)])
+    dproc = DeviceProcessor(device)
+
+    def host():
+        sd = data.SAMDataset(ds, {"prompt_type": args.prompt}, epoch_seed=0)
+        b = data.process_batch(processor, data.custom_collate([sd[i] for i in range(args.batch)]), args.prompt)
+        return data.to_device_batch(b, device)
+
+    def dev():
+        hooks = [(lambda i=i: data.seed_sample(0, i, 0)) for i in range(args.batch)]
+        return collate_device(imgs, labs, args.prompt, device, seed_hooks=hooks, processor=dproc)
+
+    out = {}
+    for name, fn in (("host_ms", host), ("hip_ms", dev)):
+        np.random.seed(0)
+        random.seed(0)
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            b = fn()
+        torch.cuda.synchronize()
+        out[name] = round((time.perf_counter() - t0) * 1e3 / reps, 2)
+        out["gt_" + name[:-3]] = b["gt_u8"]
+    same = bool(torch.equal(out.pop("gt_host").cpu(), out.pop("gt_hip").cpu()))
+    out.update({"images": args.batch, "gt_identical": same,
+                "note": "per batch, outside the timed step; host = SAMDataset+collate+SamProcessor+H2D"})
+    log(f"data path: host {out['host_ms']} ms, HIP {out['hip_ms']} ms per {args.batch} images")
+    return out
 
 
 def cpu_baseline(args, batch_cpu):
@@ -246,6 +290,10 @@ def main():
         masks = predict_masks(model, vb)
         val_dice = round(mean_dice(class_confusion(masks, vb["gt_u8"], vb["mask_values"])), 5)
 
+    data_path = None
+    if args.data_path and rank == 0:
+        data_path = time_data_path(args, device, processor)
+
     cpu = None
     if args.cpu_baseline and rank == 0 and world == 1:
         try:
@@ -266,6 +314,7 @@ def main():
                        "parallelism": f"dp{world}", "exec": "eager" if args.eager else "hipgraph"},
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
             "val_dice": val_dice,
+            "data_path": data_path,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
