@@ -126,6 +126,16 @@ def make_batch(args, rank, device, processor):
     return data.process_batch(processor, batch, args.prompt)
 
 
+def workload_name(args) -> str:
+    short = args.model.rsplit("/", 1)[-1]
+    desc = f"{short}, --prompt={args.prompt}, --top={bool(args.top)}, bf16, batch {args.batch}/GPU"
+    if short == "sam-vit-base" and args.prompt == "bboxes":
+        return f"BASELINE configs[{2 if args.top else 1}]: {desc}"
+    if short == "sam-vit-large" and args.prompt == "points" and args.top:
+        return f"BASELINE configs[3] (per-GPU slice of batch 32 over 8 GPUs): {desc}"
+    return desc
+
+
 def time_data_path(args, device, processor, reps=3):
     """Outside the timed step: one batch (B images, prompts, gt, pixel_values) built by the reference's host
     data path (SAMDataset with scipy components + custom_collate + SamProcessor, then the H2D copy) vs the
@@ -188,7 +198,7 @@ def cpu_baseline(args, batch_cpu):
     n_prompts = int(one["gt_u8"].shape[1])
     return {"value": round(args.cpu_steps / dt, 5), "unit": "imgs/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of batch 1 ({n_prompts} box prompts), fp32, "
+            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of batch 1 ({n_prompts} {args.prompt}), fp32, "
                       f"oracle/step_ref.py on {ncores} host threads"}
 
 
@@ -306,10 +316,10 @@ def main():
             "metric": METRIC, "value": round(value, 4), "unit": "imgs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": f"synthetic OCT-like 496x512 label maps -> 1024x1024 processed images, {N} box prompts/image "
-                    f"(batch max), random-init weights (seed 0)",
-            "config": {"workload": "BASELINE configs[2]: sam-vit-base, --prompt=bboxes, --top=True, bf16, "
-                                   f"batch {args.batch}/GPU", "model": args.model, "global_batch": args.batch * world,
+            "data": f"synthetic OCT-like 496x512 label maps -> 1024x1024 processed images, {N} "
+                    f"{'point' if args.prompt == 'points' else 'box'} prompts/image (batch max), random-init "
+                    f"weights (seed 0)",
+            "config": {"workload": workload_name(args), "model": args.model, "global_batch": args.batch * world,
                        "prompts_per_image": N, "prompt": args.prompt, "top": bool(args.top),
                        "parallelism": f"dp{world}", "exec": "eager" if args.eager else "hipgraph"},
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
