@@ -56,13 +56,15 @@ def test_encoder_parity(cuda, models):
     assert err < 3e-2, err
 
 
-@pytest.mark.parametrize("prompt", ["boxes", "points"])
+@pytest.mark.parametrize("prompt", ["boxes", "points", "both"])
 def test_decoder_forward_backward(cuda, models, prompt):
     ours, hf, hfb = models
     px, boxes, pts = _inputs(cuda, seed=3)
     with torch.no_grad():
         emb = hf.vision_encoder(px).last_hidden_state
-    kw = dict(input_boxes=boxes) if prompt == "boxes" else dict(input_points=pts)
+    # "both": a box and a point per prompt (BASELINE configs[4]'s mixed prompts; 8 decoder tokens)
+    kw = {"boxes": dict(input_boxes=boxes), "points": dict(input_points=pts),
+          "both": dict(input_boxes=boxes, input_points=pts)}[prompt]
     out_ref = hf(image_embeddings=emb, multimask_output=False, **kw)
     out = ours(image_embeddings=emb, multimask_output=False, **kw)
     assert out.pred_masks.shape == out_ref.pred_masks.shape
