@@ -111,6 +111,9 @@ _SIGNATURES = {
     "octsam_topo_bwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                   c_void_p, c_float, c_void_p, c_void_p]),
     "octsam_w2_host": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, ctypes.c_double, c_void_p, c_void_p]),
+    "octsam_topo_host": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                   c_int32, c_int32, ctypes.c_double, ctypes.c_double, c_int32, c_void_p,
+                                   c_void_p]),
     "octsam_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                               c_float, c_float, c_float, c_void_p, c_void_p]),
 }

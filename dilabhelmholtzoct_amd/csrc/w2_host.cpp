@@ -120,15 +120,79 @@ extern "C" int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_h
     if (j >= 0) {
       const float e0 = b - d2_host[2 * j], e1 = d - d2_host[2 * j + 1];
       const float M = std::fmax(std::fabs(e0), std::fabs(e1));
-      const float coef = (float)(q * std::pow((double)M, q - 1.0));
+      const float coef = q == 2.0 ? 2.0f * M : (float)(q * std::pow((double)M, q - 1.0));  // (same bits)
       grad_d1_host[2 * i] = coef * (std::fabs(e0) == M ? sgn(e0) : 0.0f);
       grad_d1_host[2 * i + 1] = coef * (std::fabs(e1) == M ? sgn(e1) : 0.0f);
     } else {
       const float M = diag_dist(b, d);
-      const float coef = (float)(q * std::pow((double)M, q - 1.0));
+      const float coef = q == 2.0 ? 2.0f * M : (float)(q * std::pow((double)M, q - 1.0));  // (same bits)
       grad_d1_host[2 * i] = coef * 0.5f * sgn(b - d);
       grad_d1_host[2 * i + 1] = coef * 0.5f * sgn(d - b);
     }
   }
+  return 0;
+}
+
+// All loss entries of one step in one call (the host half of topo_loss, topological_loss.py:68-96):
+// per entry e (maps entry_maps[entry_off[e] .. entry_off[e+1])), the W_q cost between the pred diagram
+// (map k) and the gt diagram (map Kn + k), tot = float32(sum of the entry's costs), loss += tot^(1/q);
+// d loss / d pred-map value accumulated into dpred [Kn, nvals] in the same order and precision as the
+// Python path it replaces (costs summed in double, the float32 products of numpy 2's promotion rules).
+extern "C" int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const float* vals, int32_t Kn,
+                                int32_t max_pairs, int32_t nvals, const int32_t* entry_maps,
+                                const int32_t* entry_off, int32_t n_entries, int32_t feat_col, double q,
+                                double lamda, int32_t want_grad, double* loss_out, float* dpred) {
+  if (!pairs || !cnt || !vals || !entry_maps || !entry_off || !loss_out || Kn <= 0 || n_entries <= 0 ||
+      (want_grad && !dpred) || feat_col < 0 || feat_col > 1)
+    return 1;
+  if (want_grad)
+    for (long long i = 0; i < (long long)Kn * nvals; ++i) dpred[i] = 0.0f;
+  std::vector<float> d1, d2, g;
+  std::vector<double> costs;
+  double total = 0.0;
+  for (int e = 0; e < n_entries; ++e) {
+    costs.clear();
+    const int e0 = entry_off[e], e1 = entry_off[e + 1];
+    std::vector<std::vector<float>> grads;
+    for (int t = e0; t < e1; ++t) {
+      const int k = entry_maps[t];
+      if (k < 0 || k >= Kn) return 1;
+      const int n = cnt[k * 3 + feat_col], m = cnt[(Kn + k) * 3 + feat_col];
+      if (n > max_pairs || m > max_pairs || cnt[k * 3 + 2] || cnt[(Kn + k) * 3 + 2]) return 1;
+      d1.resize(2 * (size_t)n);
+      d2.resize(2 * (size_t)m);
+      const int32_t* p1 = pairs + (size_t)k * max_pairs * 2;
+      const int32_t* p2 = pairs + (size_t)(Kn + k) * max_pairs * 2;
+      const float* v1 = vals + (size_t)k * nvals;
+      const float* v2 = vals + (size_t)(Kn + k) * nvals;
+      for (int i = 0; i < n; ++i) { d1[2 * i] = v1[p1[2 * i]]; d1[2 * i + 1] = v1[p1[2 * i + 1]]; }
+      for (int j = 0; j < m; ++j) { d2[2 * j] = v2[p2[2 * j]]; d2[2 * j + 1] = v2[p2[2 * j + 1]]; }
+      g.assign(2 * (size_t)n, 0.0f);
+      double c = 0.0;
+      if (octsam_w2_host(n ? d1.data() : nullptr, n, m ? d2.data() : nullptr, m, q, &c, n ? g.data() : nullptr))
+        return 1;
+      costs.push_back(c);
+      grads.push_back(g);
+    }
+    double s = 0.0;
+    for (double c : costs) s += c;  // Python sum() over floats, left to right
+    const double tot = (double)(float)s;
+    total += std::pow(tot, 1.0 / q);
+    if (want_grad) {
+      const double dd = tot > 0 ? (1.0 / q) * std::pow(tot, 1.0 / q - 1.0) : std::numeric_limits<double>::infinity();
+      // numpy 2 (NEP 50): python-float scale * float32 gradient is computed in float32
+      const float scale = (float)(lamda / n_entries * dd);
+      for (int t = e0; t < e1; ++t) {
+        const int k = entry_maps[t];
+        const int n = cnt[k * 3 + feat_col];
+        const int32_t* p1 = pairs + (size_t)k * max_pairs * 2;
+        const std::vector<float>& gg = grads[t - e0];
+        float* dp = dpred + (size_t)k * nvals;
+        for (int i = 0; i < n; ++i) dp[p1[2 * i]] += scale * gg[2 * i];
+        for (int i = 0; i < n; ++i) dp[p1[2 * i + 1]] += scale * gg[2 * i + 1];
+      }
+    }
+  }
+  *loss_out = lamda * total / n_entries;
   return 0;
 }

@@ -241,47 +241,38 @@ def topo_device_forward(masks: torch.Tensor, gt_u8: torch.Tensor, midx: torch.Te
     return (p0 if feat_d == 0 else p1), cnt, both.view(2 * Kn, interp * interp)
 
 
+@functools.lru_cache(maxsize=64)
+def _entry_csr(entries, maps):
+    """Loss entries as CSR over map positions (int32 map indices, offsets) for octsam_topo_host."""
+    pos = {m: i for i, m in enumerate(maps)}
+    flat = np.array([pos[m] for e in entries for m in e], dtype=np.int32)
+    off = np.zeros(len(entries) + 1, dtype=np.int32)
+    off[1:] = np.cumsum([len(e) for e in entries])
+    return flat, off
+
+
 def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entries, maps, *, lamda=0.1, feat_d=1,
               loss_q=2, want_grad=True):
     """Host half: W2 between the H_feat_d diagrams of pred and gt per loss entry (topological_loss.py:68-96,
-    torch_topological WassersteinDistance(q) -> exact OT, restated in octsam_w2_host). Returns the loss
-    (float) and d loss / d pred-map values [Kn, interp^2] (float32; None without want_grad)."""
+    torch_topological WassersteinDistance(q) -> exact OT, restated in octsam_w2_host), all entries in one
+    C call (octsam_topo_host). Returns the loss (float) and d loss / d pred-map values [Kn, interp^2]
+    (float32; None without want_grad)."""
     Kn = len(maps)
     if cnt_h[:, 2].any():
         raise RuntimeError("persistence pair buffer overflow; raise max_pairs")
-    col = 0 if feat_d == 0 else 1
-
-    def diagram(k):
-        n = cnt_h[k, col]
-        pr = pairs_h[k, :n]
-        v = vals_h[k]
-        return np.stack([v[pr[:, 0]], v[pr[:, 1]]], 1) if n else np.zeros((0, 2), np.float32), pr
-
-    pos = {m: i for i, m in enumerate(maps)}
-    dpred = np.zeros((Kn, vals_h.shape[1]), np.float32) if want_grad else None
-    total = 0.0
-    for e in entries:
-        costs, grads = [], []
-        for m in e:
-            k = pos[m]
-            d1, pr1 = diagram(k)
-            d2, _ = diagram(Kn + k)
-            c, g = K.w2_host(d1, d2, float(loss_q))
-            costs.append(c)
-            grads.append((k, pr1, g))
-        tot = float(np.float32(sum(costs)))
-        w = tot ** (1.0 / loss_q)
-        total += w
-        if want_grad:
-            # d(tot^(1/q)) / d tot  (inf * 0 -> nan at tot == 0, as torch's pow backward would give)
-            dd = (1.0 / loss_q) * (tot ** (1.0 / loss_q - 1.0)) if tot > 0 else float("inf")
-            for k, pr1, g in grads:
-                if len(pr1) == 0:
-                    continue
-                scale = lamda / len(entries) * dd
-                np.add.at(dpred[k], pr1[:, 0], (scale * g[:, 0]).astype(np.float32))
-                np.add.at(dpred[k], pr1[:, 1], (scale * g[:, 1]).astype(np.float32))
-    return lamda * total / len(entries), dpred
+    flat, off = _entry_csr(tuple(tuple(e) for e in entries), tuple(maps))
+    pairs_c = np.ascontiguousarray(pairs_h, dtype=np.int32)
+    cnt_c = np.ascontiguousarray(cnt_h, dtype=np.int32)
+    vals_c = np.ascontiguousarray(vals_h, dtype=np.float32)
+    loss = np.zeros(1, np.float64)
+    dpred = np.zeros((Kn, vals_c.shape[1]), np.float32) if want_grad else None
+    rc = _lib.load().octsam_topo_host(pairs_c.ctypes.data, cnt_c.ctypes.data, vals_c.ctypes.data, Kn,
+                                      pairs_c.shape[1], vals_c.shape[1], flat.ctypes.data, off.ctypes.data,
+                                      len(entries), 0 if feat_d == 0 else 1, float(loss_q), float(lamda),
+                                      int(want_grad), loss.ctypes.data,
+                                      dpred.ctypes.data if want_grad else None)
+    _lib.check(rc, "octsam_topo_host")
+    return float(loss[0]), dpred
 
 
 def topo_device_backward(masks: torch.Tensor, midx: torch.Tensor, dp: torch.Tensor, dmask: torch.Tensor, *,

@@ -288,6 +288,14 @@ int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32_t K, int32
  * and d cost / d d1 [n,2]. */
 int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_host, int32_t m, double q, double* cost_host,
                    float* grad_d1_host);
+/* The whole host half of topo_loss for one step: pairs [2Kn, max_pairs, 2] / cnt [2Kn, 3] / vals [2Kn, nvals]
+ * as produced by octsam_cubical_ph on the Kn pred maps then the Kn gt maps; loss entries given as map lists
+ * (entry_maps, CSR offsets entry_off [n_entries + 1]); feat_col 0 = H0, 1 = H1. Writes lamda * mean over
+ * entries of (sum of the entry's W_q costs)^(1/q) and, if want_grad, d loss / d pred values dpred [Kn, nvals]
+ * (topological_loss.py:68-96). Returns nonzero on bad arguments or a pair-buffer overflow. */
+int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const float* vals, int32_t Kn, int32_t max_pairs,
+                     int32_t nvals, const int32_t* entry_maps, const int32_t* entry_off, int32_t n_entries,
+                     int32_t feat_col, double q, double lamda, int32_t want_grad, double* loss_out, float* dpred);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam step over a flat fp32 buffer (ref:octsam/models/training_utils.py:31,68):
