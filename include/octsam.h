@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 5
+#define OCTSAM_ABI_VERSION 6
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1

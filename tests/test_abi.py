@@ -36,7 +36,7 @@ def test_binding_table_matches_header():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.octsam_abi_version() == 5
+    assert lib.octsam_abi_version() == 6
     assert isinstance(lib.octsam_last_error(), (bytes, type(None)))
 
 
