@@ -86,7 +86,7 @@ class FusedTrainStep:
         gt = st.gt_u8.reshape(B * N, H, W)
         masks, dpart = postproc_forward(low.view(B * N, 256, 256), st.crop, st.orig, gt)
         st.masks = masks.view(B, N, H, W)
-        st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), dpart)
+        st.dpart = dpart
         st.topo_dev = None
         if self.topological and self.lamda != 0.0:
             entries, maps, midx = topo_index(B, N, self.topo_mode, st.global_batch, masks.device)
@@ -98,6 +98,12 @@ class FusedTrainStep:
                         h.copy_(d, non_blocking=True)
                 else:
                     st.topo_out = (pairs, cnt, vals)
+
+    def _phase_f2(self, st):
+        """DiceCE loss and its gradient. Runs after the persistence and its D2H copies, so in graph mode the
+        host's W2 work overlaps it (the host waits on an event between the two graphs)."""
+        B, N, H, W = st.masks.shape
+        st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
 
     def _topo_host(self, st, backward):
         """-> topo loss (float); in backward mode also fills the device (eager) / pinned (graph) gradient."""
@@ -162,6 +168,7 @@ class FusedTrainStep:
         self._phase_e(st)
         self._finish_pending()
         self._phase_f(st, backward)
+        self._phase_f2(st)
         st.topo_val = self._topo_host(st, backward)
         self._phase_b(st, backward)
         return st.loss_out
@@ -190,7 +197,7 @@ class FusedTrainStep:
         if st.pinned is None:  # no host phase: the pinned topo scalar stays 0
             st.pinned = ()
         st.topo_pinned = torch.zeros(1, dtype=torch.float64, pin_memory=True)
-        ge, gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        ge, gf, gf2, gb = (torch.cuda.CUDAGraph() for _ in range(4))
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -199,6 +206,8 @@ class FusedTrainStep:
             pool = ge.pool()
             with torch.cuda.graph(gf, stream=s, pool=pool, capture_error_mode="relaxed"):
                 self._phase_f(st, True)
+            with torch.cuda.graph(gf2, stream=s, pool=pool, capture_error_mode="relaxed"):
+                self._phase_f2(st)
             with torch.cuda.graph(gb, stream=s, pool=pool, capture_error_mode="relaxed"):
                 self._phase_b(st, True)
         torch.cuda.current_stream(dev).wait_stream(s)
@@ -206,7 +215,7 @@ class FusedTrainStep:
         if st.pinned == ():
             st.pinned = None
             st.topo_dev = None
-        self._g = (key, ge, gf, gb, st, torch.cuda.Event())
+        self._g = (key, ge, gf, gf2, gb, st, torch.cuda.Event())
 
     def _graph_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                 global_batch):
@@ -215,12 +224,14 @@ class FusedTrainStep:
         if self._g is None or self._g[0] != key:
             self._capture(key, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                           global_batch)
-        _, ge, gf, gb, st, ev = self._g
+        _, ge, gf, gf2, gb, st, ev = self._g
         ge.replay()
         self._finish_pending()
         gf.replay()
         if st.pinned is not None:
             ev.record()
+        gf2.replay()  # DiceCE backward runs on the GPU while the host computes W2 below
+        if st.pinned is not None:
             ev.synchronize()  # the persistence pairs are in the pinned buffers
         loss = self._topo_host(st, True) if st.pinned is not None else 0.0
         if st.pinned is not None:
