@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--batch", type=int, default=8, help="images per GPU")
     p.add_argument("--model", default="facebook/sam-vit-base")
-    p.add_argument("--prompt", default="bboxes", choices=["bboxes", "points"])
+    p.add_argument("--prompt", default="bboxes", choices=["bboxes", "points", "both"])
     p.add_argument("--top", type=int, default=1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle step (rank 0, N=1)")
     p.add_argument("--cpu-steps", type=int, default=2)
@@ -131,6 +131,8 @@ def workload_name(args) -> str:
     desc = f"{short}, --prompt={args.prompt}, --top={bool(args.top)}, bf16, batch {args.batch}/GPU"
     if short == "sam-vit-base" and args.prompt == "bboxes":
         return f"BASELINE configs[{2 if args.top else 1}]: {desc}"
+    if args.prompt == "both":
+        return f"BASELINE configs[4] prompt mode (box + point per component) on {desc}"
     if short == "sam-vit-large" and args.prompt == "points" and args.top:
         return f"BASELINE configs[3] (per-GPU slice of batch 32 over 8 GPUs): {desc}"
     return desc

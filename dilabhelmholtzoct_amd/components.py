@@ -134,27 +134,41 @@ def collate_device_end(state: dict, n_target: int | None = None, processor=None)
     dev, prompt_type, seed_hooks = state["device"], state["prompt_type"], state["seed_hooks"]
     cc = state["dc"].assign(state["cc"], n_target=n_target)
     B, H, W = state["cc"]["shape"]
-    comp_h = cc["comp"].cpu().numpy() if prompt_type == "points" else None
-    prompts = []
+    comp_h = cc["comp"].cpu().numpy() if prompt_type in ("points", "both") else None
+    boxes_l, points_l = [], []
     for b in range(B):
         if seed_hooks is not None:
             seed_hooks[b]()
         if prompt_type == "points":
-            prompts.append(point_prompts(cc["stats"][b], comp_h[b]))
+            points_l.append(point_prompts(cc["stats"][b], comp_h[b]))
+        elif prompt_type == "both":  # per component: bbox draws, then the point draw
+            bx, pt = [], []
+            for n in range(cc["ncomp"][b]):
+                bx += bbox_prompts(cc["stats"][b][n:n + 1], H, W)
+                pt += point_prompts(cc["stats"][b][n:n + 1], np.where(comp_h[b] == n, 0, -1))
+            boxes_l.append(bx)
+            points_l.append(pt)
         else:
-            prompts.append(bbox_prompts(cc["stats"][b], H, W))
+            boxes_l.append(bbox_prompts(cc["stats"][b], H, W))
     N = cc["N"]
-    shape = (B, N, 1, 2) if prompt_type == "points" else (B, N, 4)
-    prompt = np.zeros(shape, dtype=np.int64)
     mask_values = torch.zeros(B, N, dtype=torch.uint8)
+    kw = {}
+    for key, lst, tail in (("input_boxes", boxes_l, (4,)), ("input_points", points_l, (1, 2))):
+        if not lst:
+            continue
+        arr = np.zeros((B, N) + tail, dtype=np.int64)
+        for b in range(B):
+            n = cc["ncomp"][b]
+            if n:
+                arr[b, :n] = np.asarray(lst[b], dtype=np.int64).reshape((n,) + tail)
+        kw[key] = arr
     for b in range(B):
         n = cc["ncomp"][b]
         if n:
-            prompt[b, :n] = np.asarray(prompts[b], dtype=np.int64).reshape((n,) + shape[2:])
             mask_values[b, :n] = torch.from_numpy(cc["values"][b])
     proc = processor if processor is not None else DeviceProcessor(dev)
-    key = "input_points" if prompt_type == "points" else "input_boxes"
-    out = proc(state["images"].to(dev), **{key: prompt})
+    out = proc(state["images"].to(dev), **kw)
+    prompt = kw["input_boxes"] if "input_boxes" in kw else kw["input_points"]
     out["gt_u8"] = cc["gt"]
     out["mask_values"] = mask_values
     out["prompt_raw"] = torch.from_numpy(prompt)

@@ -115,6 +115,26 @@ class SAMDataset(torch.utils.data.Dataset):
             gt_masks.append(np.where(labeled == c + 1, 1.0, 0.0))
         return bboxes, gt_masks, values
 
+    def get_bboxes_points_and_gt_masks(self, ground_truth_mask):
+        """``--prompt=both`` (build extension for BASELINE configs[4]; the reference CLI has bboxes or points):
+        per component, the jittered bbox (4 np.random draws) and then one random pixel (random.randrange)."""
+        bboxes, points, gt_masks, values = [], [], [], []
+        H, W = ground_truth_mask.shape
+        for v, labeled, c in self._components(ground_truth_mask):
+            values.append(v)
+            y_idx, x_idx = np.where(labeled == c + 1)
+            x_min, x_max = np.min(x_idx), np.max(x_idx)
+            y_min, y_max = np.min(y_idx), np.max(y_idx)
+            x_min = max(0, x_min + np.random.randint(-10, 10))
+            x_max = min(W, x_max + np.random.randint(-10, 10))
+            y_min = max(0, y_min + np.random.randint(-10, 10))
+            y_max = min(H, y_max + np.random.randint(-10, 10))
+            bboxes.append([x_min, y_min, x_max, y_max])
+            k = random.randrange(0, len(x_idx))
+            points.append([[x_idx[k], y_idx[k]]])
+            gt_masks.append(np.where(labeled == c + 1, 1.0, 0.0))
+        return bboxes, points, gt_masks, values
+
     def get_points_and_gt_masks(self, ground_truth_mask):
         points, gt_masks, values = [], [], []
         for v, labeled, c in self._components(ground_truth_mask):
@@ -135,6 +155,9 @@ class SAMDataset(torch.utils.data.Dataset):
         gt = np.array(item["label"])
         if self.config.get("prompt_type") == "points":
             return [image, *self.get_points_and_gt_masks(gt)]
+        if self.config.get("prompt_type") == "both":
+            bboxes, points, gt_masks, values = self.get_bboxes_points_and_gt_masks(gt)
+            return [image, bboxes, gt_masks, values, points]
         return [image, *self.get_bboxes_and_gt_masks(gt)]
 
 
@@ -145,6 +168,9 @@ def custom_collate(data):
     gt_masks = pad_sequence([torch.tensor(np.array(d[2])) for d in data], batch_first=True)
     mask_values = pad_sequence([torch.tensor(d[3]) for d in data], batch_first=True)
     prompt = pad_sequence([torch.tensor(d[1]) for d in data], batch_first=True)
+    if len(data[0]) == 5:  # --prompt=both: boxes, then points
+        points = pad_sequence([torch.tensor(d[4]) for d in data], batch_first=True)
+        return [images, prompt, gt_masks, mask_values, points]
     return [images, prompt, gt_masks, mask_values]
 
 
@@ -156,9 +182,11 @@ def make_processor():
 
 def process_batch(processor, batch, prompt_type: str = "bboxes"):
     """training_utils.py:46-53 host part: processor call; returns a dict of CPU tensors."""
-    image, prompt, gt_masks, mask_values = batch
+    image, prompt, gt_masks, mask_values = batch[:4]
     if prompt_type == "points":
         inputs = processor(image, input_points=prompt, return_tensors="pt")
+    elif prompt_type == "both":
+        inputs = processor(image, input_boxes=prompt, input_points=batch[4], return_tensors="pt")
     else:
         inputs = processor(image, input_boxes=prompt, return_tensors="pt")
     out = dict(inputs)
@@ -171,10 +199,12 @@ def process_batch_device(processor, batch, prompt_type: str = "bboxes"):
     """process_batch with the image path on the GPU (preprocess.DeviceProcessor: Pillow-exact resize +
     normalise + pad as one HIP kernel, bit-identical to SamProcessor's pixel_values); prompts, sizes and gt
     stay host tensors like process_batch's, pixel_values is already on the processor's device."""
-    image, prompt, gt_masks, mask_values = batch
+    image, prompt, gt_masks, mask_values = batch[:4]
     images = image.to(processor.device, non_blocking=True)
     if prompt_type == "points":
         out = processor(images, input_points=prompt)
+    elif prompt_type == "both":
+        out = processor(images, input_boxes=prompt, input_points=batch[4])
     else:
         out = processor(images, input_boxes=prompt)
     out["gt_u8"] = gt_masks.round().clamp(0, 1).to(torch.uint8)

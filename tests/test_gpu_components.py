@@ -38,7 +38,7 @@ def test_components_match_reference_golden(cuda, prompt):
     assert np.array_equal(out["mask_values"].numpy(), G[f"{prompt}_mask_values"])
 
 
-@pytest.mark.parametrize("prompt", ["bboxes", "points"])
+@pytest.mark.parametrize("prompt", ["bboxes", "points", "both"])
 def test_components_match_host_path(cuda, prompt):
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.components import collate_device
@@ -50,8 +50,9 @@ def test_components_match_host_path(cuda, prompt):
     labs = np.stack([np.array(ds[i]["label"]) for i in range(4)])
     hooks = [lambda i=i: data.seed_sample(2, i, 5) for i in range(4)]
     got = collate_device(imgs, labs, prompt, cuda, seed_hooks=hooks)
-    key = "input_points" if prompt == "points" else "input_boxes"
-    assert torch.equal(got[key], want[key])
+    keys = {"points": ["input_points"], "bboxes": ["input_boxes"], "both": ["input_boxes", "input_points"]}[prompt]
+    for key in keys:
+        assert torch.equal(got[key], want[key]), key
     assert torch.equal(got["gt_u8"].cpu(), want["gt_u8"])
     assert torch.equal(got["mask_values"], want["mask_values"])
     assert torch.equal(got["pixel_values"].cpu(), want["pixel_values"])

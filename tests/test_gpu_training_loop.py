@@ -25,7 +25,7 @@ def _run(cuda, gpu_processor, gpu_components, data_seed, prompt="bboxes"):
                     device=cuda)
 
 
-@pytest.mark.parametrize("data_seed,prompt", [(0, "bboxes"), (None, "points")])
+@pytest.mark.parametrize("data_seed,prompt", [(0, "bboxes"), (None, "points"), (0, "both")])
 def test_training_loop_host_vs_device_data_path(cuda, data_seed, prompt):
     runs = {"host": _run(cuda, False, False, data_seed, prompt),
             "hip processor": _run(cuda, True, False, data_seed, prompt),
