@@ -106,16 +106,28 @@ def bbox_prompts(stats: np.ndarray, H: int, W: int) -> list:
     return out
 
 
-def point_prompts(stats: np.ndarray, comp_b: np.ndarray) -> list:
-    """get_points_and_gt_masks (training_utils.py:417-434) for one sample: random.randrange over the
-    component's pixels in raster order; comp_b = that sample's rank map [H, W] (host)."""
-    W = comp_b.shape[1]
-    flat = comp_b.reshape(-1)
-    out = []
-    for n, row in enumerate(stats):
-        k = random.randrange(0, int(row[4]))
-        idx = int(np.flatnonzero(flat == n)[k])
-        out.append([[np.int64(idx % W), np.int64(idx // W)]])
+def _kth_pixels(cc: dict, ks: list, W: int) -> list:
+    """[[x, y]] of the k-th pixel (raster order, the reference's np.where order) of every component: one
+    stable device sort of the pixels by (image, component rank), then a gather at the component's offset."""
+    comp = cc["comp"]
+    B = comp.shape[0]
+    hw = comp.shape[1] * comp.shape[2]
+    maxc = max(max(cc["ncomp"]), 1)
+    key = (comp.view(B, hw).long() + torch.arange(B, device=comp.device).view(B, 1) * maxc).view(-1)
+    order = torch.sort(key, stable=True).indices
+    starts, flat = [], 0
+    for b in range(B):
+        cnt = cc["stats"][b][:, 4] if cc["ncomp"][b] else np.zeros(0, np.int64)
+        off = flat + np.concatenate([[0], np.cumsum(cnt)[:-1]]) if len(cnt) else np.zeros(0, np.int64)
+        starts.append(off + np.asarray(ks[b], dtype=np.int64))
+        flat += hw
+    pos = torch.from_numpy(np.concatenate(starts).astype(np.int64)).to(comp.device)
+    pix = (order[pos] % hw).cpu().numpy() if len(pos) else np.zeros(0, np.int64)
+    out, i = [], 0
+    for b in range(B):
+        n = cc["ncomp"][b]
+        out.append([[[np.int64(p % W), np.int64(p // W)]] for p in pix[i:i + n]])
+        i += n
     return out
 
 
@@ -134,22 +146,24 @@ def collate_device_end(state: dict, n_target: int | None = None, processor=None)
     dev, prompt_type, seed_hooks = state["device"], state["prompt_type"], state["seed_hooks"]
     cc = state["dc"].assign(state["cc"], n_target=n_target)
     B, H, W = state["cc"]["shape"]
-    comp_h = cc["comp"].cpu().numpy() if prompt_type in ("points", "both") else None
-    boxes_l, points_l = [], []
-    for b in range(B):
+    need_pts = prompt_type in ("points", "both")
+    boxes_l, points_l, ks = [], [], []
+    for b in range(B):  # the reference's draws, in its order; pixels are looked up on the device below
         if seed_hooks is not None:
             seed_hooks[b]()
-        if prompt_type == "points":
-            points_l.append(point_prompts(cc["stats"][b], comp_h[b]))
-        elif prompt_type == "both":  # per component: bbox draws, then the point draw
-            bx, pt = [], []
-            for n in range(cc["ncomp"][b]):
-                bx += bbox_prompts(cc["stats"][b][n:n + 1], H, W)
-                pt += point_prompts(cc["stats"][b][n:n + 1], np.where(comp_h[b] == n, 0, -1))
-            boxes_l.append(bx)
-            points_l.append(pt)
-        else:
-            boxes_l.append(bbox_prompts(cc["stats"][b], H, W))
+        st_b = cc["stats"][b]
+        bx, kk = [], []
+        for n in range(cc["ncomp"][b]):
+            if prompt_type in ("bboxes", "both"):
+                bx += bbox_prompts(st_b[n:n + 1], H, W)
+            if need_pts:
+                kk.append(random.randrange(0, int(st_b[n, 4])))
+        boxes_l.append(bx)
+        ks.append(kk)
+    if need_pts:
+        points_l = _kth_pixels(cc, ks, W)
+    if prompt_type == "points":
+        boxes_l = []
     N = cc["N"]
     mask_values = torch.zeros(B, N, dtype=torch.uint8)
     kw = {}
