@@ -89,9 +89,6 @@ _SIGNATURES = {
     "octsam_dec_i2t_bwd_partials": (c_int64, [c_int32, c_int32, c_int32]),
     "octsam_dec_i2t_bwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                      c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
-    "octsam_mask_dot_fwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
-    "octsam_mask_dot_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
-                                      c_void_p, c_void_p]),
     "octsam_upmask_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "octsam_upmask_bwd_workspace": (c_int64, [c_int32, c_int32]),
     "octsam_upmask_set_grid": (None, [c_int32, c_int32]),
@@ -99,6 +96,8 @@ _SIGNATURES = {
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_postproc_fwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                       c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
+    "octsam_dice_partials": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_int32, c_void_p]),
+    "octsam_confusion": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
     "octsam_dice_reduce": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "octsam_dicece_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_float, c_float,
                                     c_void_p, c_void_p, c_int32, c_void_p]),
@@ -114,7 +113,7 @@ _SIGNATURES = {
     "octsam_topo_host": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                    c_int32, c_int32, ctypes.c_double, ctypes.c_double, c_int32, c_void_p,
                                    c_void_p]),
-    "octsam_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
+    "octsam_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, ctypes.c_double, ctypes.c_double, c_float,
                               c_float, c_float, c_float, c_void_p, c_void_p]),
 }
 

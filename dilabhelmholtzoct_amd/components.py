@@ -22,6 +22,13 @@ import torch
 from . import _lib
 
 MAX_COMPONENTS = 1024
+MAX_PIXELS = 1 << 24  # root keys pack (value << 24 | pixel index)
+
+
+class ComponentLimitError(ValueError):
+    """A batch exceeds the device path's limits (> MAX_COMPONENTS components in a label map, or
+    H*W >= MAX_PIXELS); the reference has neither limit, so train.training builds such a batch on the host
+    path (SAMDataset + scipy) instead."""
 
 
 class DeviceComponents:
@@ -49,6 +56,8 @@ class DeviceComponents:
             raise ValueError(f"labels on {labels.device}, components on {self.device}")
         labels = labels.contiguous()
         B, H, W = labels.shape
+        if H * W >= MAX_PIXELS:
+            raise ComponentLimitError(f"label maps of {H}x{W} pixels exceed the device path's 2^24 limit")
         dev = self.device
         parent = torch.empty(B * H * W, device=dev, dtype=torch.int32)
         roots = torch.empty(B, self.maxc, device=dev, dtype=torch.int32)
@@ -57,7 +66,7 @@ class DeviceComponents:
                   _lib.ptr(nroots))
         counts = nroots.cpu().numpy()
         if int(counts.max()) > self.maxc:
-            raise ValueError(f"a label map has {int(counts.max())} components (> {self.maxc})")
+            raise ComponentLimitError(f"a label map has {int(counts.max())} components (> {self.maxc})")
         keys = roots.cpu().numpy()
         sorted_roots = np.zeros((B, self.maxc), dtype=np.int32)
         values = []
@@ -146,7 +155,10 @@ def collate_device_end(state: dict, n_target: int | None = None, processor=None)
     dev, prompt_type, seed_hooks = state["device"], state["prompt_type"], state["seed_hooks"]
     cc = state["dc"].assign(state["cc"], n_target=n_target)
     B, H, W = state["cc"]["shape"]
+    # SAMDataset.__getitem__ (training_utils.py:442-447): "points" -> points, anything else -> boxes;
+    # "both" (configs[4]) adds a point after each box
     need_pts = prompt_type in ("points", "both")
+    need_boxes = prompt_type != "points"
     boxes_l, points_l, ks = [], [], []
     for b in range(B):  # the reference's draws, in its order; pixels are looked up on the device below
         if seed_hooks is not None:
@@ -154,7 +166,7 @@ def collate_device_end(state: dict, n_target: int | None = None, processor=None)
         st_b = cc["stats"][b]
         bx, kk = [], []
         for n in range(cc["ncomp"][b]):
-            if prompt_type in ("bboxes", "both"):
+            if need_boxes:
                 bx += bbox_prompts(st_b[n:n + 1], H, W)
             if need_pts:
                 kk.append(random.randrange(0, int(st_b[n, 4])))
@@ -162,7 +174,7 @@ def collate_device_end(state: dict, n_target: int | None = None, processor=None)
         ks.append(kk)
     if need_pts:
         points_l = _kth_pixels(cc, ks, W)
-    if prompt_type == "points":
+    if not need_boxes:
         boxes_l = []
     N = cc["N"]
     mask_values = torch.zeros(B, N, dtype=torch.uint8)

@@ -8,16 +8,16 @@
 
 namespace {
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, long long n, float beta1, float beta2, float eps, float wd,
-                            float step_size, float bc2_sqrt, bf16* __restrict__ pb) {
+                            float* __restrict__ v, long long n, float omb1, float beta2, float omb2, float eps,
+                            float wd, float step_size, float bc2_sqrt, bf16* __restrict__ pb) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float pv = p[i];
   float gv = g[i];
   if (wd != 0.0f) gv = gv + wd * pv;
   float mv = m[i];
-  mv = mv + (1.0f - beta1) * (gv - mv);  // torch.lerp(m, g, 1-beta1), weight < 0.5 branch
-  float vv = v[i] * beta2 + (1.0f - beta2) * gv * gv;
+  mv = mv + omb1 * (gv - mv);  // torch.lerp(m, g, 1-beta1), weight < 0.5 branch
+  float vv = v[i] * beta2 + omb2 * gv * gv;  // mul_(beta2).addcmul_(g, g, value=1-beta2)
   float denom = sqrtf(vv) / bc2_sqrt + eps;
   pv = pv + (-step_size) * (mv / denom);
   p[i] = pv;
@@ -32,13 +32,15 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16* __restrict__
 }
 }  // namespace
 
-extern "C" int octsam_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
-                           float beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
+extern "C" int octsam_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double beta1,
+                           double beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
                            void* params_bf16, void* stream) {
   OCTSAM_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && n > 0, "octsam_adam: bad args");
+  // 1 - beta in double, then rounded: the scalars torch.optim.Adam hands its fp32 kernels
+  const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, params, grads,
-                     exp_avg, exp_avg_sq, n, beta1, beta2, eps, weight_decay, step_size, bias_correction2_sqrt,
-                     (bf16*)params_bf16);
+                     exp_avg, exp_avg_sq, n, omb1, (float)beta2, omb2, eps, weight_decay, step_size,
+                     bias_correction2_sqrt, (bf16*)params_bf16);
   OCTSAM_LAUNCH_CHECK("octsam_adam");
   return 0;
 }

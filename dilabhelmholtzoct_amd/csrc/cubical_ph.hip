@@ -101,7 +101,14 @@ __device__ __forceinline__ int uf_find(u16* parent, int a) {
 
 constexpr int NP2 = 8192;        // sort width (edges; vertices + pixels)
 constexpr int MAXN = 4352;       // node arrays (vertices, pixels + exterior), u16
-constexpr int REC_CAP = 1024;
+// Record capacities of the positive-persistence merges, per dimension, from the map size bound (<= 63x63):
+//   H0 pairs are born at regional minima (8-connected plateaus), pairwise non-8-adjacent: <= ceil(H/2)ceil(W/2) <= 1024
+//   H1 pairs die at regional maxima (4-connected plateaus), pairwise non-4-adjacent:     <= ceil(H*W/2)      <= 1985
+// so no map of an accepted size can overflow (a 50x50 checkerboard has 1152 H1 pairs).
+constexpr int REC0 = 1024;
+constexpr int REC1 = 2048;
+__device__ __forceinline__ int rec_base(int d) { return d ? REC0 : 0; }
+__device__ __forceinline__ int rec_cap(int d) { return d ? REC1 : REC0; }
 
 struct Smem {
   uint64_t keys[NP2];  // sort buffer; after the edge sort: epos u32[NP2] | merge logs u32[nv] | u32[npix]
@@ -112,10 +119,10 @@ struct Smem {
       u16 vrank[MAXN];   // vertex id -> rank
       u16 prank[MAXN];   // pixel -> rank
     } uf;
-    struct {
-      uint64_t key[2][REC_CAP];  // destroyer key (value bits << 32 | position / pixel)
-      int c[2][REC_CAP];         // creator: cell position, then top-coface pixel
-      float cv[2][REC_CAP];      // creator value
+    struct {  // dimension d's records at [rec_base(d), rec_base(d) + rec_cap(d))
+      uint64_t key[REC0 + REC1];  // destroyer key (value bits << 32 | position / pixel)
+      int c[REC0 + REC1];         // creator: cell position, then top-coface pixel
+      float cv[REC0 + REC1];      // creator value
     } rec;
   } u;
   u16 vinv[MAXN];  // rank -> vertex id
@@ -356,9 +363,9 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
       }
       if (keep) {
         const int r = atomicAdd(&s.nrec[d], 1);
-        if (r < REC_CAP) {
-          s.u.rec.key[d][r] = key;
-          s.u.rec.c[d][r] = cpos;
+        if (r < rec_cap(d)) {
+          s.u.rec.key[rec_base(d) + r] = key;
+          s.u.rec.c[rec_base(d) + r] = cpos;
         }
       }
     }
@@ -366,18 +373,18 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
   __syncthreads();
   // creator cells -> top-dimensional cofaces and their values
   for (int d = 0; d < 2; ++d) {
-    const int n = min(s.nrec[d], REC_CAP);
+    const int n = min(s.nrec[d], rec_cap(d)), o = rec_base(d);
     for (int i = tid; i < n; i += NTHR) {
-      const int c = top_coface(m, s.u.rec.c[d][i]);
-      s.u.rec.c[d][i] = c;
-      s.u.rec.cv[d][i] = s.vals[c];
+      const int c = top_coface(m, s.u.rec.c[o + i]);
+      s.u.rec.c[o + i] = c;
+      s.u.rec.cv[o + i] = s.vals[c];
     }
   }
   __syncthreads();
   PH_STAMP(6);
   if (tid == 0) {
-    if (s.nrec[0] > REC_CAP) s.overflow |= 1;
-    if (s.nrec[1] > REC_CAP) s.overflow |= 2;
+    if (s.nrec[0] > REC0) s.overflow |= 1;
+    if (s.nrec[1] > REC1) s.overflow |= 2;
     counts[3 * map + 0] = min(s.nrec[0], max_pairs);
     counts[3 * map + 1] = min(s.nrec[1], max_pairs);
     counts[3 * map + 2] = (s.overflow || s.nrec[0] > max_pairs || s.nrec[1] > max_pairs) ? 1 : 0;
@@ -385,16 +392,16 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
   // 4. rank pairs: (persistence desc, destroyer key asc) -- a total order, so the output does not depend on
   //    the record order; persistence in double like gudhi
   for (int d = 0; d < 2; ++d) {
-    const int n = min(s.nrec[d], REC_CAP);
+    const int n = min(s.nrec[d], rec_cap(d)), o = rec_base(d);
     int* out = d == 0 ? pairs0 : pairs1;
     for (int i = tid; i < n; i += NTHR) {
-      const uint64_t ki = s.u.rec.key[d][i];
-      const int ci = s.u.rec.c[d][i];
-      const double pi = (double)unord_bits((uint32_t)(ki >> 32)) - (double)s.u.rec.cv[d][i];
+      const uint64_t ki = s.u.rec.key[o + i];
+      const int ci = s.u.rec.c[o + i];
+      const double pi = (double)unord_bits((uint32_t)(ki >> 32)) - (double)s.u.rec.cv[o + i];
       int rank = 0;
       for (int j = 0; j < n; ++j) {
-        const uint64_t kj = s.u.rec.key[d][j];
-        const double pj = (double)unord_bits((uint32_t)(kj >> 32)) - (double)s.u.rec.cv[d][j];
+        const uint64_t kj = s.u.rec.key[o + j];
+        const double pj = (double)unord_bits((uint32_t)(kj >> 32)) - (double)s.u.rec.cv[o + j];
         rank += (pj > pi) || (pj == pi && kj < ki);
       }
       if (rank < max_pairs) {

@@ -121,6 +121,64 @@ __global__ __launch_bounds__(256) void postproc_fwd_kernel(const float* __restri
     part[((long long)m * gridDim.x + blockIdx.x) * 3 + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
 }
 
+// Dice partial sums of already post-processed masks (the drop-in DiceCELoss on [B, N, H, W] logits):
+// part[m][blk][3] = (sum p*t, sum t, sum p) over the blk-th contiguous chunk of map m, float4 loads.
+__global__ __launch_bounds__(256) void dice_partials_kernel(const float* __restrict__ x, const uint8_t* __restrict__ gt,
+                                                            long long HW, long long chunk, float* __restrict__ part) {
+  __shared__ float red[3][4];
+  const int m = blockIdx.y, tid = threadIdx.x;
+  const long long lo = (long long)blockIdx.x * chunk, hi = min(HW, lo + chunk);
+  const float* xm = x + (long long)m * HW;
+  const uint8_t* tm = gt + (long long)m * HW;
+  float si = 0.0f, st = 0.0f, sp = 0.0f;
+  for (long long e = lo + tid; e < hi; e += 256) {
+    const float t = (float)tm[e];
+    const float pr = 1.0f / (1.0f + __expf(-xm[e]));
+    si += pr * t;
+    st += t;
+    sp += pr;
+  }
+  si = wave_sum(si); st = wave_sum(st); sp = wave_sum(sp);
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane == 0) { red[0][wave] = si; red[1][wave] = st; red[2][wave] = sp; }
+  __syncthreads();
+  if (tid < 3)
+    part[((long long)m * gridDim.x + blockIdx.x) * 3 + tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+}
+
+// Per-map binary confusion counts of (x > 0) == (sigmoid(x) > 0.5) vs gt (evaluate_metrics,
+// ref:octsam/models/training_utils.py:126-156): counts[m] += (tp, fp, fn, tn), integer atomics (exact,
+// order-independent). One workgroup per (chunk, map), 16-B loads of 4 logits + 4 gt bytes per lane.
+__global__ __launch_bounds__(256) void confusion_kernel(const float* __restrict__ x, const uint8_t* __restrict__ gt,
+                                                        long long HW, long long chunk,
+                                                        unsigned long long* __restrict__ counts) {
+  __shared__ unsigned red[4][4];
+  const int m = blockIdx.y, tid = threadIdx.x;
+  const long long lo = (long long)blockIdx.x * chunk, hi = min(HW, lo + chunk);
+  const float* xm = x + (long long)m * HW;
+  const uint8_t* tm = gt + (long long)m * HW;
+  unsigned tp = 0, fp = 0, fn = 0, tn = 0;
+  for (long long e = lo + tid; e < hi; e += 256) {
+    const bool p = xm[e] > 0.0f, t = tm[e] != 0;
+    tp += p & t;
+    fp += p & !t;
+    fn += !p & t;
+    tn += !p & !t;
+  }
+  unsigned v[4] = {tp, fp, fn, tn};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  }
+  if ((tid & 63) == 0)
+    for (int k = 0; k < 4; ++k) red[k][tid >> 6] = v[k];
+  __syncthreads();
+  if (tid < 4)
+    atomicAdd(counts + 4 * m + tid,
+              (unsigned long long)(red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]));
+}
+
 // per-map dice sums -> dice loss per map, and the per-map gradient coefficients
 // coef[m] = (c1, c2): d(mean dice)/dx = (c1 * t + c2) * p (1 - p)
 __global__ __launch_bounds__(256) void dice_reduce_kernel(const float* __restrict__ part, int M, int nblk,
@@ -358,6 +416,36 @@ extern "C" int octsam_postproc_fwd(const float* lowres, int32_t M, int32_t S, in
   hipLaunchKernelGGL(postproc_fwd_kernel, dim3(ngrp, M), dim3(256), 0, (hipStream_t)stream, lowres, pp, out, gt,
                      dice_part);
   OCTSAM_LAUNCH_CHECK("octsam_postproc_fwd");
+  return 0;
+}
+
+extern "C" int octsam_dice_partials(const float* masks, const uint8_t* gt, int32_t M, int64_t HW, float* dice_part,
+                                    int32_t nblk, void* stream) {
+  OCTSAM_CHECK_ARG(masks && gt && dice_part && M > 0 && HW > 0 && nblk > 0 && M <= 65535,
+                   "octsam_dice_partials: bad args");
+  const long long chunk = (HW + nblk - 1) / nblk;
+  hipLaunchKernelGGL(dice_partials_kernel, dim3(nblk, M), dim3(256), 0, (hipStream_t)stream, masks, gt, (long long)HW,
+                     chunk, dice_part);
+  OCTSAM_LAUNCH_CHECK("octsam_dice_partials");
+  return 0;
+}
+
+extern "C" int octsam_confusion(const float* masks, const uint8_t* gt, int32_t M, int64_t HW, uint64_t* counts,
+                                void* stream) {
+  OCTSAM_CHECK_ARG(masks && gt && counts && M >= 0 && HW > 0 && M <= 65535, "octsam_confusion: bad args");
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(counts, 0, (size_t)M * 4 * sizeof(uint64_t), s);
+  if (e != hipSuccess) {
+    octsam::set_error("octsam_confusion: memset failed: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  const long long nb = (HW + 4095) / 4096;
+  const int nblk = (int)(nb < 64 ? nb : 64);
+  const long long chunk = (HW + nblk - 1) / nblk;
+  hipLaunchKernelGGL(confusion_kernel, dim3(nblk, M), dim3(256), 0, s, masks, gt, (long long)HW, chunk,
+                     (unsigned long long*)counts);
+  OCTSAM_LAUNCH_CHECK("octsam_confusion");
   return 0;
 }
 

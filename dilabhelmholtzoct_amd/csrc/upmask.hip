@@ -6,7 +6,7 @@
 // backward reads up1 and d masks, recomputes the ConvT2 product, and writes d up1 plus fixed-order
 // partials of d W2, d b2 and d hyper.
 //
-// Layout: up1 bf16 [P * 16384, 64] in the blocked order of the ConvT GEMMs (mask_head.hip): row =
+// Layout: up1 bf16 [P * 16384, 64] in the blocked order of the ConvT GEMMs (decoder.py): row =
 // (p, y1, x1, dy1, dx1), up2 column n = (dy2, dx2, c) -> pixel y = 4 y1 + 2 dy1 + dy2, x = 4 x1 + 2 dx1 + dx2.
 // A tile = 128 consecutive rows = (p, y1, half h of the x1 range), i.e. the mask block rows 4 y1 .. 4 y1 + 3,
 // columns 128 h .. 128 h + 127. Wave w owns tile rows 32 w .. 32 w + 31 (two 16-row MFMA blocks).

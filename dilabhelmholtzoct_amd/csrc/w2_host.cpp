@@ -18,6 +18,10 @@
 
 #include "../../include/octsam.h"
 
+namespace octsam {
+void set_error(const char* fmt, ...);  // api.cpp: the thread-local message behind octsam_last_error()
+}
+
 namespace {
 
 // e-maxx Hungarian for a rectangular matrix (n rows <= m cols, row-major with stride m), minimisation;
@@ -72,7 +76,10 @@ inline float sgn(float x) { return (x > 0.0f) - (x < 0.0f); }
 
 extern "C" int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_host, int32_t m, double q,
                               double* cost_host, float* grad_d1_host) {
-  if (n < 0 || m < 0 || !cost_host || (n > 0 && (!d1_host || !grad_d1_host)) || (m > 0 && !d2_host)) return 1;
+  if (n < 0 || m < 0 || !cost_host || (n > 0 && (!d1_host || !grad_d1_host)) || (m > 0 && !d2_host)) {
+    octsam::set_error("octsam_w2_host: bad arguments (n=%d, m=%d, null pointer for a non-empty diagram?)", n, m);
+    return 1;
+  }
   for (int i = 0; i < 2 * n; ++i) grad_d1_host[i] = 0.0f;
   std::vector<float> dg1(n), dg2(m);
   for (int i = 0; i < n; ++i) dg1[i] = powq(diag_dist(d1_host[2 * i], d1_host[2 * i + 1]), q);
@@ -143,8 +150,11 @@ extern "C" int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const 
                                 const int32_t* entry_off, int32_t n_entries, int32_t feat_col, double q,
                                 double lamda, int32_t want_grad, double* loss_out, float* dpred) {
   if (!pairs || !cnt || !vals || !entry_maps || !entry_off || !loss_out || Kn <= 0 || n_entries <= 0 ||
-      (want_grad && !dpred) || feat_col < 0 || feat_col > 1)
+      (want_grad && !dpred) || feat_col < 0 || feat_col > 1) {
+    octsam::set_error("octsam_topo_host: bad arguments (Kn=%d, n_entries=%d, feat_col=%d, want_grad=%d)", Kn,
+                      n_entries, feat_col, want_grad);
     return 1;
+  }
   if (want_grad)
     for (long long i = 0; i < (long long)Kn * nvals; ++i) dpred[i] = 0.0f;
   std::vector<float> d1, d2, g;
@@ -156,9 +166,16 @@ extern "C" int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const 
     std::vector<std::vector<float>> grads;
     for (int t = e0; t < e1; ++t) {
       const int k = entry_maps[t];
-      if (k < 0 || k >= Kn) return 1;
+      if (k < 0 || k >= Kn) {
+        octsam::set_error("octsam_topo_host: entry %d names map %d outside [0, %d)", e, k, Kn);
+        return 1;
+      }
       const int n = cnt[k * 3 + feat_col], m = cnt[(Kn + k) * 3 + feat_col];
-      if (n > max_pairs || m > max_pairs || cnt[k * 3 + 2] || cnt[(Kn + k) * 3 + 2]) return 1;
+      if (n > max_pairs || m > max_pairs || cnt[k * 3 + 2] || cnt[(Kn + k) * 3 + 2]) {
+        octsam::set_error("octsam_topo_host: map %d pair buffer overflow (pred %d, gt %d pairs, max_pairs %d)", k, n,
+                          m, max_pairs);
+        return 1;
+      }
       d1.resize(2 * (size_t)n);
       d2.resize(2 * (size_t)m);
       const int32_t* p1 = pairs + (size_t)k * max_pairs * 2;
@@ -170,7 +187,7 @@ extern "C" int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const 
       g.assign(2 * (size_t)n, 0.0f);
       double c = 0.0;
       if (octsam_w2_host(n ? d1.data() : nullptr, n, m ? d2.data() : nullptr, m, q, &c, n ? g.data() : nullptr))
-        return 1;
+        return 1;  // message set by octsam_w2_host
       costs.push_back(c);
       grads.push_back(g);
     }

@@ -5,7 +5,7 @@ Its parameters live in ONE flat fp32 buffer (fp32 master weights; ``flat_b16`` b
 ``flat_grad``), laid out so that projections applied to the same input are adjacent and run as one
 GEMM ([t2i.k | i2t.q | t2i.v] per block, [final.k | final.v]); ConvTranspose2d weights are stored as
 [c_in][dy][dx][c_out] so the two upscaling convolutions are plain GEMMs whose outputs stay in a
-"blocked" pixel order (see mask_head.hip). The nn.Parameters HF code and checkpoints see are views of
+"blocked" pixel order (see upmask.hip). The nn.Parameters HF code and checkpoints see are views of
 that buffer (the ConvT ones permuted views), so state_dict keys/shapes are HF's.
 
 Layer 0 shares the per-image tensors across the image's prompts (repeat_interleave at

@@ -60,13 +60,23 @@ def splitk_reduce(partials: torch.Tensor, out: torch.Tensor, splits: int, beta: 
     return out
 
 
-def cubical_ph(maps: torch.Tensor, max_pairs: int = 1024):
+def ph_max_pairs(H: int, W: int) -> int:
+    """Pair-buffer length that no [H, W] map can overflow: finite H0 pairs are born at regional minima
+    (pairwise non-8-adjacent, <= ceil(H/2)*ceil(W/2)) and H1 pairs die at regional maxima (pairwise
+    non-4-adjacent, <= ceil(H*W/2)); the kernel's record capacities cover both for every accepted size."""
+    return (H * W + 1) // 2
+
+
+def cubical_ph(maps: torch.Tensor, max_pairs: int | None = None):
     """Persistence pairs of every [H, W] map in ``maps`` ([nmaps, H, W] fp32, device).
+    max_pairs defaults to ph_max_pairs(H, W) (cannot overflow).
 
     Returns (pairs0, pairs1, essential, counts) int32 device tensors; see octsam_cubical_ph."""
     _require_cuda(maps)
     maps = maps.contiguous().float()
     nmaps, H, W = maps.shape
+    if max_pairs is None:
+        max_pairs = ph_max_pairs(H, W)
     dev = maps.device
     pairs0 = torch.empty((nmaps, max_pairs, 2), dtype=torch.int32, device=dev)
     pairs1 = torch.empty((nmaps, max_pairs, 2), dtype=torch.int32, device=dev)
@@ -229,18 +239,6 @@ def i2t_bwd(q, ldq, q_rep, k, v, P, Tk, L, dout, lddo, dq, lddq):
     splitk_reduce(part.view(nb, -1), red, nb)
     red = red.view(P, 2, Tk, 128)
     return red[:, 0], red[:, 1]
-
-
-def mask_dot_fwd(up2, hyper, P, ntok, masks):
-    _lib.call("octsam_mask_dot_fwd", ptr(up2), ptr(hyper), P, ntok, ptr(masks))
-    return masks
-
-
-def mask_dot_bwd(up2, up2pre, hyper, P, ntok, dmask, dup2pre, dhyper):
-    part = torch.empty((256, P * ntok * 32), device=up2.device, dtype=torch.float32)
-    _lib.call("octsam_mask_dot_bwd", ptr(up2), ptr(up2pre), ptr(hyper), P, ntok, ptr(dmask), ptr(dup2pre), ptr(part))
-    splitk_reduce(part, dhyper, 256)
-    return dup2pre, dhyper
 
 
 def upmask_fwd(up1, w2, b2, hyper, P, ntok, masks):

@@ -144,24 +144,20 @@ def dicece_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dice_part:
     return loss, dmask
 
 
-def _dice_partials(masks, gt_u8, nblk=16):
-    """Dice partial sums of an already post-processed mask tensor (drop-in path)."""
+def _dice_partials(masks, gt_u8, nblk=64):
+    """Dice partial sums of an already post-processed fp32 mask tensor (drop-in path): octsam_dice_partials."""
     B, N, H, W = masks.shape
-    # reuse the fused kernel through an identity "post-processing": not available -> compute here
-    p = torch.sigmoid(masks.float())
-    t = gt_u8.float()
-    part = torch.zeros(B * N, nblk, 3, device=masks.device, dtype=torch.float32)
-    part[:, 0, 0] = (p * t).sum((2, 3)).flatten()
-    part[:, 0, 1] = t.sum((2, 3)).flatten()
-    part[:, 0, 2] = p.sum((2, 3)).flatten()
+    part = torch.empty(B * N, nblk, 3, device=masks.device, dtype=torch.float32)
+    _lib.call("octsam_dice_partials", K.ptr(masks), K.ptr(gt_u8), B * N, H * W, K.ptr(part), nblk)
     return part
 
 
 class _DiceCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, masks, gt_u8, w_dice, w_ce):
-        part = _dice_partials(masks, gt_u8)
-        loss, dmask = dicece_forward_backward(masks.float().contiguous(), gt_u8, part, w_dice, w_ce)
+        x = masks.float().contiguous()
+        part = _dice_partials(x, gt_u8)
+        loss, dmask = dicece_forward_backward(x, gt_u8, part, w_dice, w_ce)
         ctx.save_for_backward(dmask)
         return loss[2]
 
@@ -171,9 +167,21 @@ class _DiceCEFn(torch.autograd.Function):
         return dmask * g.to(dmask.dtype), None, None, None
 
 
+def _binary_u8(target: torch.Tensor, who: str) -> torch.Tensor:
+    """0/1 targets as uint8 (the kernels' gt format); any other value raises (one device reduction + sync).
+    The reference's gt is the 0/1 component indicator (training_utils.py:389-434)."""
+    if target.dtype == torch.bool:
+        return target.to(torch.uint8).contiguous()
+    if bool(((target != 0) & (target != 1)).any()):
+        raise ValueError(f"{who}: targets must be binary (0/1); soft targets are not supported by the HIP kernels")
+    return target.to(torch.uint8).contiguous()
+
+
 class DiceCELoss:
-    """monai.losses.DiceCELoss(sigmoid=True) drop-in for binary (0/1) targets; float64 result like the
-    reference (training_utils.py:62 promotes to the float64 gt dtype)."""
+    """monai.losses.DiceCELoss(sigmoid=True) drop-in for binary (0/1) targets (anything else raises
+    ValueError); float64 result like the reference (training_utils.py:62 promotes to the float64 gt dtype).
+    N == 1: monai 1.3.0's CE is nn.CrossEntropyLoss over the single channel, i.e. 0 (the BCE branch for
+    one channel arrived in a later monai release)."""
 
     def __init__(self, sigmoid: bool = True, lambda_dice: float = 1.0, lambda_ce: float = 1.0, **kw):
         if not sigmoid or kw.get("softmax") or kw.get("to_onehot_y") or kw.get("include_background") is False:
@@ -184,8 +192,8 @@ class DiceCELoss:
         if input.shape != target.shape:
             raise ValueError(f"the number of dimensions for input and target should be the same, got "
                              f"shape {input.shape} and {target.shape}.")
-        gt = target if target.dtype == torch.uint8 else target.round().clamp(0, 1).to(torch.uint8)
-        return _DiceCEFn.apply(input, gt.contiguous(), self.lambda_dice, self.lambda_ce)
+        gt = _binary_u8(target, "DiceCELoss")
+        return _DiceCEFn.apply(input, gt, self.lambda_dice, self.lambda_ce)
 
 
 # ------------------------------------------------------------------------ topological loss
@@ -227,18 +235,27 @@ def topo_index(B: int, N: int, mode: str, global_batch: int | None, device):
 
 
 def topo_device_forward(masks: torch.Tensor, gt_u8: torch.Tensor, midx: torch.Tensor, *, interp=50, feat_d=1,
-                        max_pairs=1024, logits=True):
+                        max_pairs=None, logits=True):
     """Device half of the topological loss forward (no host sync; capturable): 50x50 align-corners
-    resampling of sigmoid(pred) and gt (topological_loss.py:33-46) and cubical persistence of both
-    (:55-63). Returns (pairs [2Kn, max_pairs, 2] of dim feat_d, counts [2Kn, 3], maps [2Kn, interp^2])."""
+    resampling of sigmoid(pred) and gt (topological_loss.py:33-46; interp=0: the maps as they are, :48-52)
+    and cubical persistence of both (:55-63). Returns (pairs [2Kn, max_pairs, 2] of dim feat_d, counts
+    [2Kn, 3], maps [2Kn, side^2]); max_pairs defaults to kernels.ph_max_pairs(side, side), which no map can
+    overflow. feat_d = 0 appends the essential class paired with the argmax pixel, as torch_topological's
+    CubicalComplex does with gudhi's infinite pairs."""
     B, N, H, W = masks.shape
+    oh, ow = (interp, interp) if interp else (H, W)
     Kn = midx.numel()
     dev = masks.device
-    both = torch.empty(2 * Kn, interp, interp, device=dev, dtype=torch.float32)
-    _lib.call("octsam_topo_down", K.ptr(masks), K.ptr(gt_u8), K.ptr(midx), Kn, H, W, interp, interp, int(logits),
+    both = torch.empty(2 * Kn, oh, ow, device=dev, dtype=torch.float32)
+    _lib.call("octsam_topo_down", K.ptr(masks), K.ptr(gt_u8), K.ptr(midx), Kn, H, W, oh, ow, int(logits),
               K.ptr(both[:Kn]), K.ptr(both[Kn:]))
     p0, p1, ess, cnt = K.cubical_ph(both, max_pairs=max_pairs)
-    return (p0 if feat_d == 0 else p1), cnt, both.view(2 * Kn, interp * interp)
+    if feat_d == 0:
+        rows = torch.arange(2 * Kn, device=dev)
+        p0[rows, cnt[:, 0].long()] = ess
+        cnt = cnt.clone()
+        cnt[:, 0] += 1
+    return (p0 if feat_d == 0 else p1), cnt, both.view(2 * Kn, oh * ow)
 
 
 @functools.lru_cache(maxsize=64)
@@ -259,7 +276,7 @@ def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entrie
     (float32; None without want_grad)."""
     Kn = len(maps)
     if cnt_h[:, 2].any():
-        raise RuntimeError("persistence pair buffer overflow; raise max_pairs")
+        raise RuntimeError("persistence pair buffer overflow: max_pairs below kernels.ph_max_pairs(interp, interp)")
     flat, off = _entry_csr(tuple(tuple(e) for e in entries), tuple(maps))
     pairs_c = np.ascontiguousarray(pairs_h, dtype=np.int32)
     cnt_c = np.ascontiguousarray(cnt_h, dtype=np.int32)
@@ -277,28 +294,62 @@ def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entrie
 
 def topo_device_backward(masks: torch.Tensor, midx: torch.Tensor, dp: torch.Tensor, dmask: torch.Tensor, *,
                          interp=50, logits=True):
-    """dmask += d topo / d masks, given d topo / d (resampled sigmoid map) dp [Kn, interp^2] (capturable)."""
+    """dmask += d topo / d masks, given d topo / d (resampled sigmoid map) dp [Kn, side^2] (capturable)."""
     B, N, H, W = masks.shape
-    _lib.call("octsam_topo_bwd", K.ptr(masks), K.ptr(midx), midx.numel(), H, W, interp, interp, int(logits),
+    oh, ow = (interp, interp) if interp else (H, W)
+    _lib.call("octsam_topo_bwd", K.ptr(masks), K.ptr(midx), midx.numel(), H, W, oh, ow, int(logits),
               K.ptr(dp), 1.0, K.ptr(dmask))
 
 
+def total_persistence_host(pairs_h, cnt_h, vals_h, entries, maps, *, col, q, lamda, dpred=None):
+    """loss_r of topological_loss.py:88-94: lamda * mean over the pred diagrams of every entry of
+    torch_topological.utils.total_persistence(diagram, p=q) = sum |death - birth|^q; its gradient is added
+    into dpred [Kn, nvals]. Off the reference's path (loss_r=False there); host numpy."""
+    pos = {m: i for i, m in enumerate(maps)}
+    ks = [pos[m] for e in entries for m in e]
+    if not ks:
+        return 0.0
+    total = 0.0
+    for k in ks:
+        pr = pairs_h[k, : cnt_h[k, col]]
+        b = vals_h[k][pr[:, 0]].astype(np.float64)
+        d = vals_h[k][pr[:, 1]].astype(np.float64)
+        diff = d - b
+        total += float(np.sum(np.abs(diff) ** q))
+        if dpred is not None and len(pr):
+            g = (lamda / len(ks)) * q * np.abs(diff) ** (q - 1) * np.sign(diff)
+            np.add.at(dpred[k], pr[:, 1], g.astype(np.float32))
+            np.add.at(dpred[k], pr[:, 0], (-g).astype(np.float32))
+    return lamda * total / len(ks)
+
+
 def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch.Tensor | None, *, lamda=0.1,
-                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=1024, logits=True,
-                          global_batch: int | None = None):
+                          interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=None, logits=True,
+                          global_batch: int | None = None, loss_r=False):
     """Topological loss value (float) and, when dmask is given, its gradient added into dmask.
-    masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64)."""
+    masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64). feat_d = 2 (the
+    reference's default) selects no pairs of a 2-D map: the loss is 0, as gudhi reports no H2 there."""
     if lamda == 0.0:
         return 0.0
+    if not 0 <= feat_d <= 2:
+        raise NotImplementedError("feat_d outside [0, 2] (unfiltered dimensions) is not supported")
+    if feat_d == 2:
+        return 0.0
     B, N, H, W = masks.shape
+    if not interp and (H * W > 4096 or (H + 1) * (W + 1) + H * W > 8192):
+        raise NotImplementedError(f"interp=0 needs maps the persistence kernel accepts (<= 64x63), got {H}x{W}")
     entries, maps, midx = topo_index(B, N, mode, global_batch, masks.device)
     if not entries:
         return 0.0
     pairs, cnt, both = topo_device_forward(masks, gt_u8, midx, interp=interp, feat_d=feat_d, max_pairs=max_pairs,
                                            logits=logits)
     host = [t.cpu() for t in (pairs, cnt, both)]  # one D2H sync per step (diagrams are tiny)
-    loss, dpred = topo_host(host[0].numpy(), host[1].numpy(), host[2].numpy(), entries, maps, lamda=lamda,
-                            feat_d=feat_d, loss_q=loss_q, want_grad=dmask is not None)
+    ph, ch, vh = (t.numpy() for t in host)
+    loss, dpred = topo_host(ph, ch, vh, entries, maps, lamda=lamda, feat_d=feat_d, loss_q=loss_q,
+                            want_grad=dmask is not None)
+    if loss_r:
+        loss += total_persistence_host(ph, ch, vh, entries, maps, col=0 if feat_d == 0 else 1, q=loss_q,
+                                       lamda=lamda, dpred=dpred)
     if dmask is not None:
         topo_device_backward(masks, midx, torch.from_numpy(dpred).to(masks.device), dmask, interp=interp,
                              logits=logits)
@@ -307,38 +358,37 @@ def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch
 
 class _TopoFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, maps, gt_u8, lamda, interp, feat_d, loss_q, mode, logits):
+    def forward(ctx, maps, gt_u8, lamda, interp, feat_d, loss_q, mode, logits, loss_r):
         x = maps.float().contiguous()
         dmask = torch.zeros_like(x)
         loss = topo_forward_backward(x, gt_u8, dmask, lamda=lamda, interp=interp, feat_d=feat_d, loss_q=loss_q,
-                                     mode=mode, logits=logits)
+                                     mode=mode, logits=logits, loss_r=loss_r)
         ctx.save_for_backward(dmask)
+        ctx.in_dtype = maps.dtype
         return torch.tensor(loss, device=x.device, dtype=torch.float32)
 
     @staticmethod
     def backward(ctx, g):
         (dmask,) = ctx.saved_tensors
-        return dmask * g, None, None, None, None, None, None, None
+        return (dmask * g).to(ctx.in_dtype), None, None, None, None, None, None, None, None
 
 
 def _as_u8(t):
-    return t if t.dtype == torch.uint8 else t.round().clamp(0, 1).to(torch.uint8).contiguous()
+    return _binary_u8(t, "topo_loss")
 
 
 def topo_loss_from_logits(masks, gt, lamda, interp=50, feat_d=1, loss_q=2, mode="first"):
     """topo_loss(sigmoid(masks.float()), gt.float(), ...) of training_utils.py:64, sigmoid fused."""
-    return _TopoFn.apply(masks, _as_u8(gt), lamda, interp, feat_d, loss_q, mode, True)
+    return _TopoFn.apply(masks, _as_u8(gt), lamda, interp, feat_d, loss_q, mode, True, False)
 
 
 def topo_loss(pred_obj, true_obj, lamda, interp=0, feat_d=2, loss_q=2, loss_r=False, mode="first"):
     """Signature of ref:octsam/models/topological_loss.py:11 on [B, N, H, W] probability maps and
-    binary targets. interp == 0 (full-resolution persistence) and loss_r are not implemented."""
+    binary targets (anything else raises ValueError). interp=0 runs the persistence on the maps as they
+    are (the kernel takes up to 64x63; larger maps raise NotImplementedError); loss_r adds the total-
+    persistence regulariser of :88-94. Returns a 0-dim float32 tensor (0.0 when lamda == 0, as :30-31)."""
     if lamda == 0.0:
         return 0.0
-    if interp == 0:
-        raise NotImplementedError("full-resolution cubical persistence (interp=0) is not supported")
-    if loss_r:
-        raise NotImplementedError("loss_r (total persistence regulariser) is not on the reference's path")
     if pred_obj.dim() != 4:
         raise ValueError("expected [B, C, H, W] maps")
-    return _TopoFn.apply(pred_obj, _as_u8(true_obj), lamda, interp, feat_d, loss_q, mode, False)
+    return _TopoFn.apply(pred_obj, _as_u8(true_obj), lamda, interp, feat_d, loss_q, mode, False, loss_r)

@@ -280,15 +280,31 @@ class SamModel(nn.Module):
     # -- weights ----------------------------------------------------------------------
     @classmethod
     def from_pretrained(cls, name_or_path: str, **kw) -> "SamModel":
-        """Build the named architecture. A local ``.pt``/``.safetensors`` state dict (HF key layout) is
-        loaded when ``state_dict_path`` is given; hub download is impossible offline, so otherwise the
-        weights are the deterministic synthetic initialisation (seed ``seed``, default 0)."""
+        """transformers' SamModel.from_pretrained(name) as the reference calls it (training_utils.py:274-275),
+        offline. Weights, in order:
+          1. ``state_dict_path=`` (a ``.pt`` / ``.safetensors`` state dict with HF keys), or a file path;
+          2. a directory with ``model.safetensors`` / ``pytorch_model.bin`` (save_pretrained layout);
+          3. a hub name found in the local HF cache (``$HF_HUB_CACHE`` or ``$HF_HOME/hub``:
+             ``models--facebook--sam-vit-base/snapshots/*/model.safetensors``);
+          4. otherwise the deterministic synthetic initialisation — silently only when ``seed=`` is given
+             (an explicit opt-in to random weights); without it a warning names the paths searched."""
         import os
-        model = cls(kw.pop("config", None) or config_for(os.path.basename(name_or_path.rstrip("/"))
-                                                          if name_or_path not in _ALL_NAMES else name_or_path))
+        import warnings
+        cfg = kw.pop("config", None)
+        seed = kw.pop("seed", None)
         path = kw.pop("state_dict_path", None)
-        if path is None and os.path.isfile(name_or_path):
-            path = name_or_path
+        arch = name_or_path if name_or_path in _ALL_NAMES else os.path.basename(name_or_path.rstrip("/"))
+        if cfg is None:
+            try:
+                cfg = config_for(arch)
+            except ValueError:
+                cfg = config_for("facebook/sam-vit-base") if path or os.path.exists(name_or_path) else None
+                if cfg is None:
+                    raise
+        model = cls(cfg)
+        searched = []
+        if path is None:
+            path = _find_weights(name_or_path, searched)
         if path:
             if path.endswith(".safetensors"):
                 from safetensors.torch import load_file
@@ -296,8 +312,16 @@ class SamModel(nn.Module):
             else:
                 sd = torch.load(path, map_location="cpu", weights_only=True)
             model.load_state_dict(sd)
+            model.weights_path = path
         else:
-            model.init_weights(seed=kw.pop("seed", 0))
+            if seed is None:
+                warnings.warn(f"SamModel.from_pretrained({name_or_path!r}): no local weights found (searched: "
+                              f"{', '.join(searched) or 'nothing'}); the hub is unreachable offline, so the "
+                              f"weights are the synthetic random initialisation (seed 0). Pass seed= to opt "
+                              f"into random weights explicitly.", UserWarning, stacklevel=2)
+                seed = 0
+            model.init_weights(seed=seed)
+            model.weights_path = None
         return model
 
     @torch.no_grad()
@@ -418,6 +442,43 @@ class SamModel(nn.Module):
 
 
 _ALL_NAMES = set()
+_WEIGHT_FILES = ("model.safetensors", "pytorch_model.bin")
+
+
+def _hf_cache_dirs():
+    import os
+    out = []
+    for var in ("HF_HUB_CACHE", "HUGGINGFACE_HUB_CACHE"):
+        if os.environ.get(var):
+            out.append(os.environ[var])
+    home = os.environ.get("HF_HOME") or os.path.join(os.path.expanduser("~"), ".cache", "huggingface")
+    out.append(os.path.join(home, "hub"))
+    return list(dict.fromkeys(out))
+
+
+def _find_weights(name_or_path: str, searched: list) -> str | None:
+    """Local weight file for a path or hub name (see SamModel.from_pretrained), or None."""
+    import glob
+    import os
+    if os.path.isfile(name_or_path):
+        return name_or_path
+    if os.path.isdir(name_or_path):
+        for f in _WEIGHT_FILES:
+            cand = os.path.join(name_or_path, f)
+            searched.append(cand)
+            if os.path.isfile(cand):
+                return cand
+        return None
+    if "/" in name_or_path:
+        repo = "models--" + name_or_path.replace("/", "--")
+        for root in _hf_cache_dirs():
+            for f in _WEIGHT_FILES:
+                pat = os.path.join(root, repo, "snapshots", "*", f)
+                searched.append(pat)
+                hits = sorted(glob.glob(pat))
+                if hits:
+                    return hits[-1]
+    return None
 
 
 def _names():

@@ -189,7 +189,8 @@ class FusedTrainStep:
             entries, maps, midx = topo_index(B, N, self.topo_mode, global_batch, dev)
             Kn = len(maps)
             if Kn:
-                st.pinned = (torch.empty((2 * Kn, 1024, 2), dtype=torch.int32, pin_memory=True),
+                mp = K.ph_max_pairs(self.interp, self.interp)
+                st.pinned = (torch.empty((2 * Kn, mp, 2), dtype=torch.int32, pin_memory=True),
                              torch.empty((2 * Kn, 3), dtype=torch.int32, pin_memory=True),
                              torch.empty((2 * Kn, self.interp * self.interp), dtype=torch.float32, pin_memory=True))
                 st.dp_pinned = torch.zeros((Kn, self.interp * self.interp), dtype=torch.float32, pin_memory=True)
@@ -330,30 +331,22 @@ def predict_masks(model: SamModel, batch: dict) -> torch.Tensor:
 @torch.no_grad()
 def class_confusion(masks: torch.Tensor, gt_u8: torch.Tensor, mask_values: torch.Tensor, num_classes: int = 14):
     """Per-class pooled (tp, fp, fn) of sigmoid(mask) > 0.5 vs gt, with the reference's early break when a
-    background-valued prompt follows the first one (training_utils.py:126-134). int64 [C, 3]."""
-    conf = torch.zeros(num_classes, 3, dtype=torch.int64)
-    pred = masks > 0.0  # sigmoid(x) > 0.5  <=>  x > 0
-    gt = gt_u8.bool()
-    tp = (pred & gt).sum((2, 3)).cpu()
-    fp = (pred & ~gt).sum((2, 3)).cpu()
-    fn = (~pred & gt).sum((2, 3)).cpu()
+    background-valued prompt follows the first one (training_utils.py:126-134). int64 [C, 3]. The counts
+    of every prompt come from the HIP kernel octsam_confusion (metrics.prompt_confusion)."""
+    from .metrics import included_prompts, prompt_confusion
+    B, N = masks.shape[:2]
+    per = prompt_confusion(masks, gt_u8).view(B, N, 4).cpu()
     mv = mask_values.cpu()
-    B, N = mv.shape
-    for b in range(B):
-        for c in range(N):
-            v = int(mv[b, c])
-            if v == 0 and c > 0:
-                break
-            conf[v, 0] += tp[b, c]
-            conf[v, 1] += fp[b, c]
-            conf[v, 2] += fn[b, c]
+    conf = torch.zeros(num_classes, 3, dtype=torch.int64)
+    for b, c in included_prompts(mv):
+        conf[int(mv[b, c])] += per[b, c, :3]
     return conf
 
 
 def mean_dice(conf: torch.Tensor) -> float:
     """'Mean dice' of training_utils.py:156,246: mean over classes of 2tp/(2tp+fp+fn) (0 if empty)."""
     d = []
-    for tp, fp, fn in conf.tolist():
+    for tp, fp, fn in conf[:, :3].tolist():
         den = 2 * tp + fp + fn
         d.append(2 * tp / den if den else 0.0)
     return sum(d) / len(d)
@@ -426,7 +419,7 @@ def _prep(ds, idx, prompt, device, device_data):
     Returns (kind, state, local N)."""
     from . import data
     if device_data and idx:
-        from .components import collate_device_begin
+        from .components import ComponentLimitError, collate_device_begin
         if ds.config.get("pseudocolor") is not None:
             raise NotImplementedError("cv2 pseudocolor maps are not available offline")
         its = [ds.dataset[i] for i in idx]
@@ -437,8 +430,11 @@ def _prep(ds, idx, prompt, device, device_data):
         hooks = None
         if ds.epoch_seed is not None:
             hooks = [(lambda i=i: data.seed_sample(ds.epoch, i, ds.epoch_seed)) for i in idx]
-        st = collate_device_begin(imgs, labs, prompt, device, hooks)
-        return "dev", st, max(st["cc"]["ncomp"])
+        try:
+            st = collate_device_begin(imgs, labs, prompt, device, hooks)
+            return "dev", st, max(st["cc"]["ncomp"])
+        except ComponentLimitError:
+            pass  # beyond the device path's limits: the reference's host path below (same draws, same batch)
     items = [ds[i] for i in idx]
     return "host", items, _n_prompts(items)
 
@@ -476,7 +472,7 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     world = dist.get_world_size(pg) if pg is not None else 1
     rank = dist.get_rank(pg) if pg is not None else 0
     device = device or torch.device("cuda", torch.cuda.current_device())
-    model = SamModel.from_pretrained(base_model, seed=config.get("seed", 0)).to(device)
+    model = SamModel.from_pretrained(base_model, **({"seed": config["seed"]} if "seed" in config else {})).to(device)
     if device.type == "cuda" and config.get("gpu_processor", True):  # image path as a HIP kernel (§8(f)1)
         from .preprocess import DeviceProcessor
         processor = DeviceProcessor(device)
@@ -534,11 +530,14 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
         torch.save(model.state_dict(), ckpt)  # training_utils.py:77 (HF state-dict keys)
     hist["checkpoint"] = ckpt
     if config.get("evaluate", True):
-        conf = evaluate_confusion(model, vds, processor, bs, prompt, world, rank, pg, device, device_data)
+        conf, metrics = evaluate_model(model, vds, processor, bs, prompt, world, rank, pg, device, device_data)
         hist["dice"] = class_dice(conf)
         hist["mean_dice"] = mean_dice(conf)
+        hist["metrics"] = metrics
         if rank == 0:
-            log(f"Mean dice: {hist['mean_dice']}")
+            m = metrics["mean"]
+            log(f"Mean_accuracy:{m['accuracy']}\nMean_iou:{m['iou']}\nMean specificity: {m['specificity']}\n"
+                f"Mean sensitivity: {m['sensitivity']}\nMean dice: {hist['mean_dice']}\nMean mAP: {m['ap']}")
     return hist
 
 
@@ -569,18 +568,34 @@ def validate_model(step: FusedTrainStep, vds, processor, bs, config, world=1, ra
 
 
 @torch.no_grad()
-def evaluate_confusion(model, vds, processor, bs, prompt, world=1, rank=0, pg=None, device=None,
-                       device_data=False):
-    """Pooled per-class (tp, fp, fn) over the validation set (evaluate_metrics, training_utils.py:113-156),
-    summed over ranks."""
-    conf = torch.zeros(14, 3, dtype=torch.int64)
+def evaluate_model(model, vds, processor, bs, prompt, world=1, rank=0, pg=None, device=None, device_data=False):
+    """evaluate_metrics (training_utils.py:113-270) over the validation set on the GPU: per-prompt confusion
+    counts (HIP), per-class pooled and per-sample IoU / accuracy / specificity / sensitivity / F1 / Dice / AP
+    (metrics.EvalAccumulator). Data parallel: the per-sample counts of all ranks are gathered, so every
+    confusion-based metric is the single-process one; the pooled AP needs every score and is computed only
+    when world == 1 (NaN otherwise). Returns (pooled (tp, fp, fn) int64 [14, 3], metrics dict)."""
+    from .metrics import EvalAccumulator
+    acc = EvalAccumulator(keep_scores=(world == 1))
     for idx in global_batches(len(vds), bs, world, rank):
         if not idx:
             continue
         prep = _prep(vds, idx, prompt, device, device_data)
         batch = _finish(prep, processor, prompt, prep[2], device)
-        conf += class_confusion(predict_masks(model, batch), batch["gt_u8"], batch["mask_values"])
-    return _collective_sum(conf, pg)
+        acc.add(predict_masks(model, batch), batch["gt_u8"], batch["mask_values"], image_index=idx)
+    if pg is not None:
+        import torch.distributed as dist
+        got = [None] * world
+        dist.all_gather_object(got, (acc.counts, acc.samples), group=pg)
+        acc.counts = [sum((g[0][v] for g in got), []) for v in range(acc.C)]
+        acc.samples = [sum((g[1][v] for g in got), []) for v in range(acc.C)]
+    return acc.pooled_confusion()[:, :3], acc.compute()
+
+
+@torch.no_grad()
+def evaluate_confusion(model, vds, processor, bs, prompt, world=1, rank=0, pg=None, device=None,
+                       device_data=False):
+    """Pooled per-class (tp, fp, fn) over the validation set (training_utils.py:113-156), all ranks."""
+    return evaluate_model(model, vds, processor, bs, prompt, world, rank, pg, device, device_data)[0]
 
 
 def class_dice(conf: torch.Tensor) -> list:
@@ -591,12 +606,21 @@ def class_dice(conf: torch.Tensor) -> list:
     return out
 
 
-def main(argv=None):
-    """CLI mirror of ref:octsam/models/training.py (same flags and defaults; W&B, display and pseudocolour
-    options are accepted and ignored). --synthetic K trains on K synthetic OCT-like images instead of a
-    save_to_disk dataset."""
+def _bool_flag(v) -> bool:
+    if isinstance(v, bool):
+        return v
+    s = str(v).strip().lower()
+    if s in ("true", "1", "yes", "y", "on"):
+        return True
+    if s in ("false", "0", "no", "n", "off"):
+        return False
     import argparse
-    import datetime
+    raise argparse.ArgumentTypeError(f"expected True or False, got {v!r}")
+
+
+def build_parser():
+    """argparse of ref:octsam/models/training.py:20-93 (same flags and defaults)."""
+    import argparse
     p = argparse.ArgumentParser()
     p.add_argument("--project_name", type=str, default="OCT-Mikhail-experiments")
     p.add_argument("--entity", type=str, default="dilab-helmholtz")
@@ -621,9 +645,19 @@ def main(argv=None):
     p.add_argument("--display_name", type=str, default="")
     p.add_argument("--evaluate", type=bool, default=True)
     p.add_argument("--prompt", type=str, default="bboxes")
-    p.add_argument("--top", action="store_true")
+    p.add_argument("--top", nargs="?", const=True, default=False, type=_bool_flag,
+                   help="topological loss: --top, --top=True or --top=False (README usage; the reference's "
+                        "store_true flag rejects --top=True)")
     p.add_argument("--synthetic", type=int, default=0, help="train on K synthetic images (no dataset on disk)")
-    args = p.parse_args(argv)
+    return p
+
+
+def main(argv=None):
+    """CLI mirror of ref:octsam/models/training.py (same flags and defaults; W&B, display and pseudocolour
+    options are accepted and ignored). --synthetic K trains on K synthetic OCT-like images instead of a
+    save_to_disk dataset."""
+    import datetime
+    args = build_parser().parse_args(argv)
     if args.loss != "diceCE" or args.optimizer != "adam":
         raise SystemExit("only --loss diceCE and --optimizer adam exist in the reference")
     if args.pseudocolor != "grayscale":

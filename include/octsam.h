@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 6
+#define OCTSAM_ABI_VERSION 7
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -95,11 +95,13 @@ int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t s
  *   pairs0[map][i] = (creator pixel, destroyer pixel) of finite H0 pairs, i < counts[map*3+0]
  *   pairs1[map][i] = same for H1,                                        i < counts[map*3+1]
  *   essential[map] = (creator pixel of the essential H0 class, argmax pixel)
- *   counts[map*3+2] = 1 if a pair list overflowed max_pairs (the map is then incomplete)
+ *   counts[map*3+2] = 1 if a pair list overflowed max_pairs (the map is then incomplete); with
+ *   max_pairs >= ceil(H*W/2) no map can overflow (finite H0 pairs <= ceil(H/2)*ceil(W/2), H1 pairs
+ *   <= ceil(H*W/2): births at pairwise non-adjacent regional minima / deaths at regional maxima)
  * Pixel indices are C-order flat indices into the map, exactly the index space of
  * cofaces_of_persistence_pairs(). Pairs are ordered by decreasing persistence, ties by the
  * filtration order of the destroyer cell. Zero-persistence pairs are dropped (gudhi
- * min_persistence=0). Requires H*W <= 4096 and H,W >= 1.
+ * min_persistence=0). Requires H,W >= 1, H*W <= 4096 and (H+1)*(W+1) + H*W <= 8192 (up to 64x63).
  */
 int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, int32_t W, int32_t max_pairs,
                       int32_t* pairs0, int32_t* pairs1, int32_t* essential, int32_t* counts, void* stream);
@@ -221,17 +223,8 @@ int octsam_dec_i2t_bwd(const void* q, int64_t ldq, int32_t q_rep, const float* k
                        int32_t L, const void* dout, int64_t lddo, void* dq, int64_t lddq, float* partials,
                        void* stream);
 
-/* ---------------------------------------------------------------- mask head
- * masks = hyper_in @ upscaled_embedding (hf:modeling_sam.py:523-542). up2 bf16 [P, 65536, 32] in the
- * blocked order of the two ConvTranspose2d GEMMs (pixel y = 4y1+2dy1+dy2, x = 4x1+2dx1+dx2);
- * hyper fp32 [P, ntok, 32]; masks fp32 [P, ntok, 256, 256]. Backward: dup2pre = (dmask x hyper) *
- * gelu'(up2pre) (bf16) and partials fp32 [256, P, ntok, 32] of d hyper. */
-int octsam_mask_dot_fwd(const void* up2, const float* hyper, int32_t P, int32_t ntok, float* masks, void* stream);
-int octsam_mask_dot_bwd(const void* up2, const void* up2pre, const float* hyper, int32_t P, int32_t ntok,
-                        const float* dmask, void* dup2pre, float* partials, void* stream);
-
 /* Fused upscaling tail + mask head (hf:modeling_sam.py:519-542: the second ConvTranspose2d, its GELU
- * and masks = hyper_in @ upscaled_embedding; replaces octsam_gemm (conv2) + octsam_mask_dot_* in the
+ * and masks = hyper_in @ upscaled_embedding; replaces an octsam_gemm (conv2) + a separate mask product in the
  * training step): the 32-channel 256x256 upscaled embedding is never stored.
  * up1 bf16 [P*16384, 64] (LN+GELU output of the first ConvTranspose2d, blocked row order as above);
  * w2 bf16 [64, 128] = ConvT2 weight [in][(dy2, dx2, c)]; b2 fp32 [32]; hyper fp32 [P, ntok, 32];
@@ -253,6 +246,10 @@ int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const fl
  *   mid x mid (align_corners=False) -> crop [:crop_h,:crop_w] -> bilinear to out_h x out_w, fused,
  *   torch upsample_bilinear2d index arithmetic. With gt (uint8 [M,out_h,out_w], binary) it also writes
  *   the Dice partial sums dice_part fp32 [M, nblk, 3] = (sum sigmoid(x)*t, sum t, sum sigmoid(x)).
+ * octsam_dice_partials: the same partial sums for masks that are already post-processed (fp32 [M, HW],
+ *   gt uint8 [M, HW]) -> dice_part [M, nblk, 3] (the drop-in DiceCELoss; M <= 65535).
+ * octsam_confusion: per-map binary confusion counts (evaluate_metrics, ref:octsam/models/training_utils.py:
+ *   126-156): counts uint64 [M, 4] = (tp, fp, fn, tn) of (masks > 0, i.e. sigmoid > 0.5) vs gt (overwritten).
  * octsam_dice_reduce: monai DiceLoss(sigmoid=True) per map (smooth 1e-5): dice_map double [M] and the
  *   gradient coefficients coef fp32 [M,2].
  * octsam_dicece_bwd: CrossEntropyLoss over the prompt dim N with probability targets + the Dice
@@ -263,6 +260,9 @@ int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const fl
 int octsam_postproc_fwd(const float* lowres, int32_t M, int32_t S, int32_t mid, int32_t crop_h, int32_t crop_w,
                         int32_t out_h, int32_t out_w, float* out, const uint8_t* gt, float* dice_part, int32_t nblk,
                         void* stream);
+int octsam_dice_partials(const float* masks, const uint8_t* gt, int32_t M, int64_t HW, float* dice_part, int32_t nblk,
+                         void* stream);
+int octsam_confusion(const float* masks, const uint8_t* gt, int32_t M, int64_t HW, uint64_t* counts, void* stream);
 int octsam_dice_reduce(const float* dice_part, int32_t M, int32_t nblk, double* dice_map, float* coef, void* stream);
 int octsam_dicece_bwd(const float* masks, const uint8_t* gt, const float* coef, int32_t B, int32_t N, int64_t HW,
                       float w_dice, float w_ce, float* dmask, double* ce_part, int32_t nblk, void* stream);
@@ -300,9 +300,10 @@ int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const float* vals
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam step over a flat fp32 buffer (ref:octsam/models/training_utils.py:31,68):
  * step_size = lr / (1 - beta1^t), bias_correction2_sqrt = sqrt(1 - beta2^t) computed by the caller;
- * params_bf16 (optional) receives the updated parameters in bf16. */
-int octsam_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float beta1,
-                float beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
+ * params_bf16 (optional) receives the updated parameters in bf16. beta1/beta2 are double so that 1 - beta
+ * is rounded to fp32 from the double difference, as torch forms it. */
+int octsam_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double beta1,
+                double beta2, float eps, float weight_decay, float step_size, float bias_correction2_sqrt,
                 void* params_bf16, void* stream);
 
 #ifdef __cplusplus

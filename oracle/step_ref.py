@@ -33,9 +33,10 @@ def synthetic_state_dict(base_model: str, seed: int = 0):
 
 class CpuReferenceStep:
     def __init__(self, base_model="facebook/sam-vit-base", topological=False, seed=0, lr=1e-3, weight_decay=0.0,
-                 topo_mode="first", state_dict=None, device="cpu"):
+                 topo_mode="first", state_dict=None, device="cpu", loss_device="cpu"):
         """device: where the fp32 SamModel runs (CPU for the bench baseline; a GPU only to speed up the
-        val-Dice parity test). Post-processing and losses always run on the CPU in fp32/f64."""
+        val-Dice parity test); loss_device: where the torch post-processing and losses run (fp32 / f64; the
+        persistence and the transport plan are always CPU code)."""
         from transformers import SamModel
         self.model = SamModel(hf_config(base_model)).float()
         self.model.load_state_dict(state_dict if state_dict is not None else synthetic_state_dict(base_model, seed))
@@ -47,9 +48,10 @@ class CpuReferenceStep:
         self.opt = torch.optim.Adam(self.model.mask_decoder.parameters(), lr=lr, weight_decay=weight_decay)
         self.topological = topological
         self.topo_mode = topo_mode
+        self.loss_device = torch.device(loss_device)
 
     def predict(self, batch):
-        """Post-processed fp32 logits [B, N, H, W] on the CPU (training_utils.py:56-58 / :121-125)."""
+        """Post-processed fp32 logits [B, N, H, W] on loss_device (training_utils.py:56-58 / :121-125)."""
         dev = self.device
         inputs = {"pixel_values": batch["pixel_values"].float().to(dev)}
         if "input_boxes" in batch:
@@ -57,7 +59,7 @@ class CpuReferenceStep:
         if "input_points" in batch:
             inputs["input_points"] = batch["input_points"].to(dev)
         out = self.model(**inputs, multimask_output=False)
-        masks = F.interpolate(out.pred_masks.squeeze(2).cpu(), (1024, 1024), mode="bilinear",
+        masks = F.interpolate(out.pred_masks.squeeze(2).to(self.loss_device), (1024, 1024), mode="bilinear",
                               align_corners=False)
         rh, rw = (int(v) for v in batch["reshaped_input_sizes"][0])
         oh, ow = (int(v) for v in batch["original_sizes"][0])
@@ -65,7 +67,7 @@ class CpuReferenceStep:
         return F.interpolate(masks, (oh, ow), mode="bilinear", align_corners=False)
 
     def forward_loss(self, batch):
-        gt = batch["gt_u8"].cpu().double()
+        gt = batch["gt_u8"].to(self.loss_device).double()
         masks = self.predict(batch)
         loss = dicece_ref(masks, gt)
         topo = torch.zeros((), dtype=torch.float64)

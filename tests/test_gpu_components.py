@@ -38,8 +38,9 @@ def test_components_match_reference_golden(cuda, prompt):
     assert np.array_equal(out["mask_values"].numpy(), G[f"{prompt}_mask_values"])
 
 
-@pytest.mark.parametrize("prompt", ["bboxes", "points", "both"])
+@pytest.mark.parametrize("prompt", ["bboxes", "points", "both", "boxes"])
 def test_components_match_host_path(cuda, prompt):
+    """"boxes" (any unrecognised --prompt string) means bboxes, as SAMDataset.__getitem__ decides."""
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.components import collate_device
     ds = data.synthetic_oct(seed=11, n=4)
@@ -50,7 +51,7 @@ def test_components_match_host_path(cuda, prompt):
     labs = np.stack([np.array(ds[i]["label"]) for i in range(4)])
     hooks = [lambda i=i: data.seed_sample(2, i, 5) for i in range(4)]
     got = collate_device(imgs, labs, prompt, cuda, seed_hooks=hooks)
-    keys = {"points": ["input_points"], "bboxes": ["input_boxes"], "both": ["input_boxes", "input_points"]}[prompt]
+    keys = {"points": ["input_points"], "both": ["input_boxes", "input_points"]}.get(prompt, ["input_boxes"])
     for key in keys:
         assert torch.equal(got[key], want[key]), key
     assert torch.equal(got["gt_u8"].cpu(), want["gt_u8"])
@@ -118,5 +119,20 @@ def test_components_too_many(cuda):
     from dilabhelmholtzoct_amd.components import DeviceComponents
     lab = (np.add.outer(np.arange(64), np.arange(64)) % 2).astype(np.uint8)
     lab[::2, :] = 2 + (np.arange(64) % 2)[None, :]  # stripes of isolated pixels: > 16 components
-    with pytest.raises(ValueError):
+    from dilabhelmholtzoct_amd.components import ComponentLimitError
+    with pytest.raises(ComponentLimitError):
         DeviceComponents(cuda, max_components=16)(torch.from_numpy(lab[None]).to(cuda))
+
+
+def test_training_falls_back_to_host_path_beyond_limits(cuda, monkeypatch):
+    """A label map beyond the device path's component limit is built by the host path (the reference has no
+    such limit): train._prep returns the host items instead of raising."""
+    from dilabhelmholtzoct_amd import components, data, train
+    monkeypatch.setattr(components, "MAX_COMPONENTS", 4)
+    orig = components.DeviceComponents.__init__
+    monkeypatch.setattr(components.DeviceComponents, "__init__",
+                        lambda self, device, max_components=4: orig(self, device, 4))
+    ds = data.synthetic_oct(seed=3, n=2)
+    sd = data.SAMDataset(ds, {"prompt_type": "bboxes"}, epoch_seed=1)
+    kind, state, n = train._prep(sd, [0, 1], "bboxes", cuda, True)
+    assert kind == "host" and n == max(len(state[0][3]), len(state[1][3])) > 4

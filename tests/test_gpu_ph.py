@@ -66,3 +66,32 @@ def test_ph_deterministic(cuda):
     for i in range(maps.shape[0]):
         assert torch.equal(a[0][i, : cnt[i, 0]], b[0][i, : cnt[i, 0]])
         assert torch.equal(a[1][i, : cnt[i, 1]], b[1][i, : cnt[i, 1]])
+
+
+def _adversarial(H, W):
+    """Maps at the pair-count bounds: a checkerboard (one H1 hole per interior high pixel: ~H*W/2 pairs),
+    isolated minima on the even lattice (ceil(H/2)*ceil(W/2) H0 classes) and a sigmoid-saturated
+    checkerboard with exact 0/1 plateaus."""
+    yy, xx = np.mgrid[0:H, 0:W]
+    cb = ((yy + xx) % 2).astype(np.float32)
+    minima = np.where((yy % 2 == 0) & (xx % 2 == 0), 0.0, 1.0).astype(np.float32)
+    minima += (np.random.default_rng(H * W).random((H, W)) * 1e-3).astype(np.float32) * (minima > 0)
+    sat = (1 / (1 + np.exp(-np.where(cb > 0, 120.0, -120.0)))).astype(np.float32)
+    return np.stack([cb, minima, sat])
+
+
+@pytest.mark.parametrize("H,W", [(50, 50), (64, 63), (63, 64)])
+def test_ph_max_pair_counts_no_overflow(cuda, H, W):
+    """Verdict r1: a 50x50 checkerboard has ~1150 H1 pairs, more than the old fixed 1024 records; the
+    default buffer (kernels.ph_max_pairs) must hold every map the kernel accepts, bit-exact."""
+    from dilabhelmholtzoct_amd import kernels
+    maps = _adversarial(H, W)
+    p0, p1, ess, cnt = (t.cpu().numpy() for t in kernels.cubical_ph(torch.from_numpy(maps).to(cuda)))
+    assert p1.shape[1] == kernels.ph_max_pairs(H, W)
+    for i, m in enumerate(maps):
+        ref = ph_oracle(m)
+        assert cnt[i, 2] == 0
+        assert [tuple(map(int, r)) for r in p0[i, : cnt[i, 0]]] == ref["h0"], f"map {i} H0"
+        assert [tuple(map(int, r)) for r in p1[i, : cnt[i, 1]]] == ref["h1"], f"map {i} H1"
+        assert tuple(map(int, ess[i])) == ref["essential"]
+    assert cnt[0, 1] > 1024 and cnt[1, 0] == ((H + 1) // 2) * ((W + 1) // 2) - 1

@@ -1,13 +1,19 @@
 """Val-Dice parity (BASELINE.json north_star: "val Dice within ±0.005 of the CPU reference on identical
-seeds"). Both sides start from the same synthetic weights, train K steps on the same batch with the
-topological loss on (BASELINE configs[2]: boxes, --top=True) and then score the same held-out images with
-the reference's per-class pooled Dice (training_utils.py:113-156, with its early `break`):
+seeds"). Both sides start from the same synthetic weights, train on the same BASELINE configs[2] batches
+(B = 8 OCT images, box prompts, --top=True, two alternating batches) for 24 steps, and score the same 8
+held-out images at checkpoints 0 / 8 / 16 / 24:
 
-* ours: HIP path (FusedTrainStep: bf16 MFMA encoder/decoder, fused losses, HIP Adam) + predict_masks;
-* oracle: oracle/step_ref.py (transformers SamModel fp32 — run on the GPU here only to keep the test
-  short — restated DiceCE / topo loss and torch Adam on the CPU).
+* ours: the HIP path (FusedTrainStep: bf16 MFMA encoder/decoder, fused losses, HIP Adam) + predict_masks,
+  scored by train.class_confusion / mean_dice (HIP confusion counts);
+* oracle: oracle/step_ref.py (transformers SamModel fp32 — run on the GPU here only to keep the test short —
+  restated DiceCE / topo loss, torch Adam), scored by oracle/eval_ref.py (the reference's evaluate_metrics
+  loop with its break quirk, :113-156, and sklearn confusion counts).
 
-Tolerance: |Dice_ours - Dice_ref| <= 0.005 (the north_star bar), after 0 and after K = 3 steps."""
+lr = 1e-3, the reference CLI's default (training.py --lr). Tolerance: |Dice_ours - Dice_ref| <= 0.005 at every
+checkpoint (the north_star bar). At lr = 3e-3 the fp32 trajectory is chaotic on these random-init weights:
+the same oracle under torch.autocast(bfloat16) drifts 0.043 from fp32 by step 8 (the HIP path too), so no bf16
+implementation can meet the bar there (scripts/dice_drift.py, profiles/r02_dice_drift.txt); at 1e-3 the
+autocast model stays within 0.001 and the HIP path within 0.003."""
 import pytest
 import torch
 
@@ -15,6 +21,8 @@ pytestmark = pytest.mark.gpu
 
 NAME = "facebook/sam-vit-base"
 TOL = 0.005
+LR = 1e-3
+CHECKPOINTS = (0, 8, 16, 24)
 
 
 def _batches():
@@ -25,50 +33,50 @@ def _batches():
         ds = data.synthetic_oct(seed=seed, n=n)
         sd = data.SAMDataset(ds, {"prompt_type": "bboxes"}, epoch_seed=0)
         return data.process_batch(proc, data.custom_collate([sd[i] for i in range(len(sd))]), "bboxes")
-    return mk(1000, 2), mk(999, 3)
+    return [mk(1000, 8), mk(1001, 8)], mk(999, 8)
 
 
-def _dice(masks, vb):
-    from dilabhelmholtzoct_amd.train import class_confusion, mean_dice
-    return mean_dice(class_confusion(masks, vb["gt_u8"], vb["mask_values"]))
+def _ref_dice(masks, vb):
+    import numpy as np
+    from oracle.eval_ref import evaluate_metrics_ref
+    B = masks.shape[0]
+    r = evaluate_metrics_ref([masks[b].cpu() for b in range(B)], [vb["gt_u8"][b] for b in range(B)],
+                             [vb["mask_values"][b].tolist() for b in range(B)])
+    return float(np.mean(r["category"]["dice"]))
 
 
 def test_val_dice_parity(cuda):
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.model import SamModel
-    from dilabhelmholtzoct_amd.train import FusedTrainStep, predict_masks
+    from dilabhelmholtzoct_amd.train import FusedTrainStep, class_confusion, mean_dice, predict_masks
     from oracle.step_ref import CpuReferenceStep, synthetic_state_dict
 
     state = synthetic_state_dict(NAME, seed=0)
-    train_cpu, val_cpu = _batches()
-    train, val = data.to_device_batch(train_cpu, cuda), data.to_device_batch(val_cpu, cuda)
+    trains_cpu, val_cpu = _batches()
+    trains = [data.to_device_batch(t, cuda) for t in trains_cpu]
+    val = data.to_device_batch(val_cpu, cuda)
 
     ours = SamModel(NAME)
     ours.load_state_dict(state)
     ours = ours.to(cuda)
-    step = FusedTrainStep(ours, lr=1e-3, topological=True, graphs=False)
-    ref = CpuReferenceStep(NAME, topological=True, lr=1e-3, state_dict=state, device=cuda)
-
-    def both_dice():
-        got = _dice(predict_masks(ours, val), val)
-        with torch.no_grad():
-            rmasks = ref.predict(val_cpu)
-        want = _dice(rmasks, val_cpu)
-        return got, want
+    step = FusedTrainStep(ours, lr=LR, topological=True, graphs=False)
+    ref = CpuReferenceStep(NAME, topological=True, lr=LR, state_dict=state, device=cuda, loss_device=cuda)
 
     results = []
-    got, want = both_dice()
-    results.append((0, got, want))
-    for _ in range(3):
-        step.step(train)
-        ref.step(train_cpu)
-    step.flush()
-    torch.cuda.synchronize()
-    got, want = both_dice()
-    results.append((3, got, want))
-    for k, got, want in results:
-        print(f"after {k} steps: val Dice HIP {got:.5f}  oracle {want:.5f}  diff {got - want:+.5f}")
+    for k in range(CHECKPOINTS[-1] + 1):
+        if k in CHECKPOINTS:
+            step.flush()
+            got = mean_dice(class_confusion(predict_masks(ours, val), val["gt_u8"], val["mask_values"]))
+            with torch.no_grad():
+                want = _ref_dice(ref.predict(val_cpu), val_cpu)
+            results.append((k, got, want))
+            print(f"after {k:2d} steps: val Dice HIP {got:.5f}  oracle {want:.5f}  diff {got - want:+.5f}",
+                  flush=True)
+        if k == CHECKPOINTS[-1]:
+            break
+        step.step(trains[k % 2])
+        ref.step(trains_cpu[k % 2])
     for k, got, want in results:
         assert abs(got - want) <= TOL, (k, got, want)
-    # the steps must have moved the model (else the second check repeats the first)
-    assert results[1][2] != results[0][2]
+    moved = max(abs(w - results[0][2]) for _, _, w in results)
+    assert moved >= 0.005, f"oracle Dice moved only {moved:.4f}: the checkpoints do not test training"

@@ -88,3 +88,26 @@ def test_topo_host_overflow_raises():
     cnt[0, 2] = 1
     with pytest.raises(RuntimeError):
         topo_host(pairs, cnt, vals, [[0]], [0])
+
+
+def test_topo_host_error_messages():
+    """Argument errors of the host entry points set octsam_last_error."""
+    from dilabhelmholtzoct_amd import _lib
+    lib = _lib.load()
+    pairs, cnt, vals = _case(5, 1, [2, 2])
+    flat = np.array([3], np.int32)
+    off = np.array([0, 1], np.int32)
+    loss = np.zeros(1, np.float64)
+    rc = lib.octsam_topo_host(pairs.ctypes.data, cnt.ctypes.data, vals.ctypes.data, 1, pairs.shape[1],
+                              vals.shape[1], flat.ctypes.data, off.ctypes.data, 1, 1, 2.0, 0.1, 0,
+                              loss.ctypes.data, None)
+    assert rc == 1 and b"outside" in lib.octsam_last_error()
+    cnt[1, 1] = pairs.shape[1] + 1
+    flat[0] = 0
+    rc = lib.octsam_topo_host(pairs.ctypes.data, cnt.ctypes.data, vals.ctypes.data, 1, pairs.shape[1],
+                              vals.shape[1], flat.ctypes.data, off.ctypes.data, 1, 1, 2.0, 0.1, 0,
+                              loss.ctypes.data, None)
+    assert rc == 1 and b"overflow" in lib.octsam_last_error()
+    cost = np.zeros(1, np.float64)
+    assert lib.octsam_w2_host(None, 2, None, 0, 2.0, cost.ctypes.data, None) == 1
+    assert b"octsam_w2_host" in lib.octsam_last_error()
