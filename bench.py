@@ -28,6 +28,12 @@ import torch  # noqa: E402
 
 METRIC = "train imgs/sec (1024² OCT, vit-base, top-loss on) + val Dice; 1→8 GPUs"
 MI355X_BF16_DENSE_TFLOPS = 2500.0  # /opt/skills/guides/MI355X_MICROARCH.md (dense, no sparsity)
+MI355X_HBM_GBS = 8000.0  # HBM3E peak, same guide
+# SURVEY.md §8(d) algorithmic decoder traffic per prompt: every inter-kernel image-side tensor written and
+# read once, E = 4096 tokens x 256 ch x 2 B: 12 E forward, 24 E backward
+_E = 4096 * 256 * 2
+DEC_FWD_BYTES_PER_PROMPT = 12 * _E
+DEC_BWD_BYTES_PER_PROMPT = 24 * _E
 # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x2 for
 # gfx950's half-counted wide reads + WRITE_SIZE; scripts/gpu_round.sh -> scripts/pmc_traffic.py), same bench
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_gemm8.json")
@@ -54,6 +60,9 @@ def parse():
     p.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
     p.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
     p.add_argument("--roof-steps", type=int, default=2, help="eager steps timed per GEMM launch for the roofline")
+    p.add_argument("--e2e-steps", type=int, default=10,
+                   help="steps of the end-to-end loop (a new batch per step through the HIP data path)")
+    p.add_argument("--topo-all", type=int, default=1, help="time the topo_mode='all' reading of batch_iter too")
     return p.parse_args()
 
 
@@ -118,6 +127,48 @@ class GemmEventTimer:
         return ms, n, self.flops
 
 
+class CallTimer:
+    """HIP events (torch's current stream = the launch stream of every wrapper) around each call of
+    ``owner.name`` while active; ``work(*a, **kw)`` gives the call's algorithmic FLOPs or bytes."""
+
+    def __init__(self, owner, name, work):
+        self.owner, self.name, self.work = owner, name, work
+        self.orig = getattr(owner, name)
+        self.events, self.total = [], 0.0
+        self.active = False
+
+    def __enter__(self):
+        orig = self.orig
+
+        def wrapped(*a, **kw):
+            if not self.active:
+                return orig(*a, **kw)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = orig(*a, **kw)
+            e.record()
+            self.events.append((s, e))
+            self.total += self.work(*a, **kw)
+            return out
+
+        setattr(self.owner, self.name, wrapped)
+        return self
+
+    def __exit__(self, *a):
+        setattr(self.owner, self.name, self.orig)
+
+    def result(self):
+        torch.cuda.synchronize()
+        return sum(s.elapsed_time(e) for s, e in self.events), len(self.events), self.total
+
+
+def attn_flops(qkv, out, rh, rw, *, nseq, side, heads, head_dim=64):
+    """QK^T and PV of one octsam_vit_attention launch: 4 * T^2 * head_dim * heads * nseq, T = side^2 (the
+    windowed layers' padded 14x14 windows included, as the reference computes them)."""
+    T = side * side
+    return 4.0 * T * T * head_dim * heads * nseq
+
+
 def make_batch(args, rank, device, processor):
     from dilabhelmholtzoct_amd import data
     ds = data.synthetic_oct(seed=1000 + rank, n=args.batch)
@@ -179,6 +230,101 @@ def time_data_path(args, device, processor, reps=3):
     return out
 
 
+def end_to_end(args, step, device, rank, world, pg, n_raw=4):
+    """value_end_to_end: the step fed a NEW batch every iteration, as the reference's loop is
+    (training_utils.py:41-55): uint8 images + label maps (n_raw distinct synthetic sets, re-drawn prompts
+    every epoch) -> HIP data path (components, prompts, gt, processor; components.collate_device) on a side
+    stream, overlapped with the previous step (built while the GPU runs that step's forward), then copied into
+    the captured graphs' inputs. Disk decoding of the dataset is not included (no dataset on disk)."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.components import collate_device
+    from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
+    raw = []
+    for k in range(n_raw):
+        ds = data.synthetic_oct(seed=5000 + 100 * rank + k, n=args.batch)
+        raw.append((np.stack([d["image"] for d in ds]), np.stack([d["label"] for d in ds])))
+    dproc = DeviceProcessor(device)
+    side = torch.cuda.Stream(device=device)
+    main_stream = torch.cuda.current_stream(device)
+
+    def prep(i):
+        imgs, labs = raw[i % n_raw]
+        hooks = [(lambda j=j, e=i: data.seed_sample(e, j, rank)) for j in range(args.batch)]
+        with torch.cuda.stream(side):
+            b = collate_device(imgs, labs, args.prompt, device, seed_hooks=hooks, processor=dproc)
+            b.pop("prompt_raw")
+            if world > 1:  # global-N padding (a tiny MAX all-reduce on the main process group)
+                b = _pad_global(b, pg, device)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for v in b.values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(main_stream)
+        return b, ev
+
+    def run(n):
+        nxt = prep(0)
+        for i in range(n):
+            cur, ev = nxt
+            main_stream.wait_event(ev)
+            holder = []
+            step.step(cur, between=lambda i=i: holder.append(prep(i + 1)))
+            nxt = holder[0]
+        step.flush()
+
+    log(f"rank {rank}: end-to-end warm-up (one capture per batch shape)")
+    run(2 * n_raw)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.e2e_steps)
+    torch.cuda.synchronize()
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if pg is not None:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = args.batch * world * args.e2e_steps / dt
+    log(f"rank {rank}: end-to-end {dt * 1e3 / args.e2e_steps:.2f} ms/step ({value:.1f} imgs/s)")
+    return {"value": round(value, 4), "unit": "imgs/s", "ms_per_step": round(dt * 1e3 / args.e2e_steps, 3),
+            "steps": args.e2e_steps, "distinct_raw_batches": n_raw,
+            "note": "new batch per step: uint8 images + label maps -> HIP components/prompts/gt/processor on a "
+                    "side stream overlapped with the previous step; no disk decode"}
+
+
+def _pad_global(b, pg, device):
+    import torch.distributed as dist
+    from dilabhelmholtzoct_amd import data
+    n = torch.tensor([b["gt_u8"].shape[1]], device=device)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=pg)
+    return data.pad_prompts(b, int(n.item())) if int(n.item()) > b["gt_u8"].shape[1] else b
+
+
+def topo_all_sensitivity(args, model, batch, steps=5):
+    """ms/step with the topo_mode='all' reading of torch_topological's batch_iter (every prompt's diagrams,
+    2*B*N persistence maps per step instead of 2*B; SURVEY.md §8(a) A17 — the reading is unpinned)."""
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    st = FusedTrainStep(model, lr=1e-3, topological=True, topo_mode="all", graphs=not args.eager)
+    for _ in range(2):
+        st.step(batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step(batch)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    B, N = batch["gt_u8"].shape[:2]
+    out = {"ms_per_step": round(dt * 1e3 / steps, 3), "imgs_per_s": round(B * steps / dt, 2),
+           "persistence_maps_per_step": 2 * B * N, "steps": steps}
+    log(f"topo_mode=all: {out}")
+    return out
+
+
 def cpu_baseline(args, batch_cpu):
     """CPU oracle step (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE/topo + Adam) on a
     bounded sample (1 image, all its prompts), timed on this host's cores."""
@@ -204,8 +350,37 @@ def cpu_baseline(args, batch_cpu):
                       f"oracle/step_ref.py on {ncores} host threads"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args, cmd=None) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes (one per GPU, RCCL rendezvous on
+    127.0.0.1) as children — before this process touches the GPU — relay rank 0's JSON line, return the
+    worst exit code. torchrun's own environment (WORLD_SIZE set) skips this."""
+    import subprocess
+    port = str(_free_port())
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, WORLD_SIZE=str(args.gpus), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(rcs, key=abs)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -256,19 +431,62 @@ def main():
     dt = time.perf_counter() - t0
     # Roofline of the dominant kernel: HIP events around each of its launches. Graph replays run no
     # Python, so the launches are timed in `roof_steps` eager steps of the same batch right after the
-    # timed region (same kernels, shapes and stream); rocprofv3 over the graph run must agree.
+    # timed region (same kernels, shapes and stream); rocprofv3 over the graph run must agree. The same
+    # eager steps time the encoder attention kernels, the patch embedding and the decoder fwd / bwd (the
+    # north_star's roofline split: MFMA share of encoder attention, HBM GB/s of the patch-embed/decoder path).
     timer = GemmEventTimer() if not args.no_events and args.roof_steps > 0 else None
+    split = {}
     if timer:
+        from dilabhelmholtzoct_amd import kernels as Kmod
+        from dilabhelmholtzoct_amd.decoder import MaskDecoder
+        P = args.batch * N
+        hidden = model.config.vision.hidden_size
+        timers = {
+            "attn": CallTimer(Kmod, "vit_attention", attn_flops),
+            "patch": CallTimer(Kmod, "patchify_bf16", lambda px, out: px.numel() * 4.0 + out.numel() * 2.0),
+            "dec_fwd": CallTimer(MaskDecoder, "forward_impl", lambda *a, **k: P * DEC_FWD_BYTES_PER_PROMPT),
+            "dec_bwd": CallTimer(MaskDecoder, "backward_impl", lambda *a, **k: P * DEC_BWD_BYTES_PER_PROMPT),
+        }
         graphs = step.graphs
         step.graphs = False
         timer.__enter__()
+        for t in timers.values():
+            t.__enter__()
+            t.active = True
         timer.active = True
         for _ in range(args.roof_steps):
             step.step(batch)
         step.flush()
         timer.active = False
+        for t in timers.values():
+            t.active = False
+            t.__exit__()
         timer.__exit__()
         step.graphs = graphs
+        ams, an, aflops = timers["attn"].result()
+        pms, pn, pbytes = timers["patch"].result()
+        fms, fn_, fbytes = timers["dec_fwd"].result()
+        bms, bn, bbytes = timers["dec_bwd"].result()
+        if an:
+            a_tf = aflops / (ams * 1e-3) / 1e12
+            split["encoder_attention"] = {
+                "bound": "mfma", "achieved": round(a_tf, 2), "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(a_tf / MI355X_BF16_DENSE_TFLOPS, 4), "launches": an,
+                "avg_launch_us": round(ams * 1e3 / an, 2),
+                "work": "4*T^2*head_dim*heads*sequences per launch (global T=4096, windowed T=196 padded)"}
+        if fn_ and bn:
+            dbytes = pbytes + fbytes + bbytes
+            dms = pms + fms + bms
+            gbs = dbytes / (dms * 1e-3) / 1e9
+            split["decoder_hbm"] = {
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
+                "frac": round(gbs / MI355X_HBM_GBS, 4),
+                "ms_per_step": {"patch_embed": round(pms / args.roof_steps, 3),
+                                "decoder_fwd": round(fms / args.roof_steps, 3),
+                                "decoder_bwd": round(bms / args.roof_steps, 3)},
+                "work": f"patch-embed 18 B/pixel-triple (fp32 in, bf16 out); decoder {DEC_FWD_BYTES_PER_PROMPT / 1e6:.1f} "
+                        f"MB fwd + {DEC_BWD_BYTES_PER_PROMPT / 1e6:.1f} MB bwd per prompt (SURVEY.md §8(d): 12 E + "
+                        f"24 E, E = 4096*256*2 B), {P} prompts"}
     if pg is not None:
         import torch.distributed as dist
         t = torch.tensor([dt], device=device, dtype=torch.float64)
@@ -293,14 +511,26 @@ def main():
                     "compulsory_bytes_per_launch": round(timer.bytes / n),
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}
+            roof.update(split)
+
+    e2e = None
+    if args.e2e_steps > 0 and not args.eager:
+        e2e = end_to_end(args, step, device, rank, world, pg)
+    topo_all = None
+    if args.topo_all and args.top and rank == 0 and world == 1:
+        topo_all = topo_all_sensitivity(args, model, batch)
 
     log(f"rank {rank}: {dt * 1e3 / args.steps:.2f} ms/step")
-    val_dice = None
+    val_dice = val_metrics = None
     if args.val and rank == 0:
         vb = data.to_device_batch(make_batch(argparse.Namespace(batch=args.val, prompt=args.prompt), 999, device,
                                              processor), device)
         masks = predict_masks(model, vb)
         val_dice = round(mean_dice(class_confusion(masks, vb["gt_u8"], vb["mask_values"])), 5)
+        from dilabhelmholtzoct_amd.metrics import EvalAccumulator
+        acc = EvalAccumulator()
+        acc.add(masks, vb["gt_u8"], vb["mask_values"])
+        val_metrics = {k: round(v, 5) for k, v in acc.compute()["mean"].items()}
 
     data_path = None
     if args.data_path and rank == 0:
@@ -326,7 +556,11 @@ def main():
                        "parallelism": f"dp{world}", "exec": "eager" if args.eager else "hipgraph"},
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
             "val_dice": val_dice,
+            "val_metrics_mean": val_metrics,
             "data_path": data_path,
+            "value_end_to_end": e2e["value"] if e2e else None,
+            "end_to_end": e2e,
+            "topo_mode_all": topo_all,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -60,7 +60,7 @@ class FusedTrainStep:
         self._pe = None
         self.graphs = graphs
         self.overlap = overlap and process_group is not None
-        self._g = None          # captured graphs + static tensors for one batch shape
+        self._graphs = {}       # batch shape -> captured graphs + static input copies (graph mode)
         self._pending = None    # (event, ) of an all-reduce whose Adam step has not run yet
         self._side = None
 
@@ -152,15 +152,19 @@ class FusedTrainStep:
 
     @torch.no_grad()
     def forward_backward(self, pixel_values, gt_u8, input_boxes=None, input_points=None, input_labels=None,
-                         crop=(992, 1024), orig=(496, 512), global_batch=None, backward=True):
+                         crop=(992, 1024), orig=(496, 512), global_batch=None, backward=True, between=None):
         """Returns a device float64 tensor [4] = (dice, ce, topo, total). With backward=True leaves the
         decoder gradient in mask_decoder.flat_grad. global_batch: images in the global (all-rank) batch,
-        which fixes the topological loss's batch nesting."""
+        which fixes the topological loss's batch nesting. between: optional callable run on
+        the host while the GPU works on the step (after the forward is queued)."""
         if self.graphs and backward:
             return self._graph_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop,
-                                                orig, global_batch)
-        return self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
-                                            global_batch, backward)
+                                                orig, global_batch, between)
+        out = self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
+                                           global_batch, backward)
+        if between is not None:
+            between()
+        return out
 
     def _eager_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                 global_batch, backward):
@@ -174,11 +178,17 @@ class FusedTrainStep:
         return st.loss_out
 
     def _graph_key(self, *ts):
-        return tuple((None if t is None else (tuple(t.shape), t.dtype, t.data_ptr())) for t in ts)
+        return tuple((None if t is None else (tuple(t.shape), t.dtype)) for t in ts)
 
-    def _capture(self, key, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch):
-        dev = pixel_values.device
-        self._g = None
+    MAX_GRAPHS = 8  # captured step graphs kept (one per batch shape: B, the prompt count N, prompt kind)
+
+    def _capture(self, key, inputs, crop, orig, global_batch):
+        """Capture E / F / F2 / B for one batch shape. The graphs read their own static copies of the
+        inputs (``inputs`` is cloned), so any later batch of the same shape is replayed after a copy-in."""
+        dev = inputs[0].device
+        # device copies (prompts may come as host tensors from the data path; the graphs read device memory)
+        pixel_values, gt_u8, input_boxes, input_points, input_labels = (
+            None if t is None else t.detach().to(dev, copy=True) for t in inputs)
         # one eager pass first: lazily built operand caches, tables and kernel attributes exist before capture
         self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                      global_batch, True)
@@ -216,22 +226,46 @@ class FusedTrainStep:
         if st.pinned == ():
             st.pinned = None
             st.topo_dev = None
-        self._g = (key, ge, gf, gf2, gb, st, torch.cuda.Event())
+        static = (pixel_values, gt_u8, input_boxes, input_points, input_labels)
+        g = {"graphs": (ge, gf, gf2, gb), "st": st, "ev": torch.cuda.Event(), "static": static,
+             "src": tuple(self._src_tag(t) for t in inputs)}
+        self._graphs[key] = g
+        while len(self._graphs) > self.MAX_GRAPHS:
+            self._graphs.pop(next(iter(self._graphs)))
+        return g
+
+    @staticmethod
+    def _src_tag(t):
+        return None if t is None else (t.data_ptr(), t._version, t.device)
+
+    def _copy_in(self, g, inputs):
+        """Copy a new batch into the captured graphs' static inputs (skipped for the tensors that were copied
+        last and have not changed since: same storage, same version counter)."""
+        tags = tuple(self._src_tag(t) for t in inputs)
+        for dst, src, tag, old in zip(g["static"], inputs, tags, g["src"]):
+            if src is not None and tag != old:
+                dst.copy_(src, non_blocking=True)
+        g["src"] = tags
 
     def _graph_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
-                                global_batch):
-        key = self._graph_key(pixel_values, gt_u8, input_boxes, input_points, input_labels) + (
-            tuple(crop), tuple(orig), global_batch)
-        if self._g is None or self._g[0] != key:
-            self._capture(key, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
-                          global_batch)
-        _, ge, gf, gf2, gb, st, ev = self._g
+                                global_batch, between=None):
+        inputs = (pixel_values, gt_u8, input_boxes, input_points, input_labels)
+        key = self._graph_key(*inputs) + (tuple(crop), tuple(orig), global_batch)
+        g = self._graphs.get(key)
+        if g is None:
+            g = self._capture(key, inputs, crop, orig, global_batch)
+            g["src"] = (None,) * 5  # the capture ran on clones: copy this batch in like any other
+        self._copy_in(g, inputs)
+        ge, gf, gf2, gb = g["graphs"]
+        st, ev = g["st"], g["ev"]
         ge.replay()
         self._finish_pending()
         gf.replay()
         if st.pinned is not None:
             ev.record()
         gf2.replay()  # DiceCE backward runs on the GPU while the host computes W2 below
+        if between is not None:
+            between()  # host work overlapped with the step (e.g. building the next batch on a side stream)
         if st.pinned is not None:
             ev.synchronize()  # the persistence pairs are in the pinned buffers
         loss = self._topo_host(st, True) if st.pinned is not None else 0.0
@@ -288,15 +322,16 @@ class FusedTrainStep:
         """Apply a deferred (overlapped) parameter update."""
         self._finish_pending()
 
-    def step(self, batch: dict, n_global=None):
+    def step(self, batch: dict, n_global=None, between=None):
         """batch: device tensors from data.process_batch/to_device_batch. n_global: images in the global
-        batch (data parallel; None = this rank's batch is the whole batch)."""
+        batch (data parallel; None = this rank's batch is the whole batch). between: host work to overlap
+        with the step (see forward_backward)."""
         crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
         orig = tuple(int(v) for v in batch["original_sizes"][0])
         n_local = int(batch["pixel_values"].shape[0])
         loss = self.forward_backward(batch["pixel_values"], batch["gt_u8"], input_boxes=batch.get("input_boxes"),
                                      input_points=batch.get("input_points"), input_labels=batch.get("input_labels"),
-                                     crop=crop, orig=orig, global_batch=n_global)
+                                     crop=crop, orig=orig, global_batch=n_global, between=between)
         self._launch_update(n_local, n_global)
         return loss
 

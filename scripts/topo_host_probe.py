@@ -16,5 +16,5 @@ step._topo_host = timed
 for _ in range(8): step.step(b)
 step.flush(); torch.cuda.synchronize()
 print("topo_host us per call:", [round(x * 1e6) for x in ts[-5:]])
-st = step._g[5]
+st = next(iter(step._graphs.values()))["st"]
 print("h1 counts", st.pinned[1].numpy()[:, 1].tolist())
