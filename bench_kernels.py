@@ -45,23 +45,19 @@ def main():
         lib.octsam_gemm_set_fast_path(1)
         print(json.dumps(res), flush=True)
         del A, W, out
-    for side, nseq, heads in [(64, 8, 12), (14, 200, 12)]:
+    for side, nseq, heads, hd, dt in [(64, 8, 12, 64, torch.bfloat16), (14, 200, 12, 64, torch.bfloat16),
+                                      (64, 8, 16, 80, torch.bfloat16), (14, 200, 16, 80, torch.bfloat16),
+                                      (64, 8, 16, 80, torch.float16), (14, 200, 16, 80, torch.float16)]:
         T = side * side
-        qkv = torch.randn(nseq, T, 3 * heads * 64, generator=g).to(dev, torch.bfloat16)
-        o = torch.empty(nseq, T, heads * 64, device=dev, dtype=torch.bfloat16)
-        Rh = torch.randn(2 * side - 1, 64, device=dev) * 0.02
-        fl = 4.0 * nseq * heads * T * T * 64
-        res = {"case": "vit_attention", "side": side, "nseq": nseq}
-        outs = []
-        for v in (1, 0):
-            lib.octsam_attention_set_variant(v)
-            ms = timeit(lambda: K.vit_attention(qkv, o, Rh, Rh, nseq=nseq, side=side, heads=heads))
-            res[f"v{v}"] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
-            outs.append(o.float().clone())
-        lib.octsam_attention_set_variant(1)
-        res["v1_vs_v0_maxdiff"] = (outs[0] - outs[1]).abs().max().item()
-        print(json.dumps(res), flush=True)
-
+        qkv = torch.randn(nseq, T, 3 * heads * hd, generator=g).to(dev, dt)
+        o = torch.empty(nseq, T, heads * hd, device=dev, dtype=dt)
+        Rh = torch.randn(2 * side - 1, hd, device=dev) * 0.02
+        fl = 4.0 * nseq * heads * T * T * hd
+        byts = (qkv.numel() + o.numel()) * 2
+        ms = timeit(lambda: K.vit_attention(qkv, o, Rh, Rh, nseq=nseq, side=side, heads=heads))
+        print(json.dumps({"case": "vit_attention", "side": side, "nseq": nseq, "heads": heads, "head_dim": hd,
+                          "dtype": str(dt).split(".")[-1], "us": round(ms * 1e3, 1),
+                          "tflops": round(fl / ms / 1e9, 1), "gbs": round(byts / ms / 1e6, 1)}), flush=True)
 
 if __name__ == "__main__":
     main()

@@ -45,7 +45,6 @@ _SIGNATURES = {
     "octsam_gemm": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
     "octsam_gemm_set_fast_path": (None, [c_int32]),
     "octsam_gemm_last_path": (c_int32, []),
-    "octsam_attention_set_variant": (None, [c_int32]),
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
     "octsam_cubical_ph": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
@@ -58,7 +57,7 @@ _SIGNATURES = {
     "octsam_relu_bwd": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p]),
     "octsam_group_sum": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "octsam_vit_attention": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
-                                       c_int32, c_void_p]),
+                                       c_int32, c_int32, c_void_p]),
     "octsam_axpby": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int64, c_float, c_float, c_void_p,
                                c_int32, c_void_p, c_int64, c_void_p]),
     "octsam_colsum": (c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_void_p]),

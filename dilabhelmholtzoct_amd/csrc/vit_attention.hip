@@ -4,250 +4,72 @@
 // with get_rel_pos / get_decomposed_rel_pos (:729-801). The [B*h, T, T] bias tensor that HF
 // materialises (805 MB per image for a global vit-b layer) is never formed:
 //
-//   s[q,k] = (q/8)·k + rel_h[q, kh] + rel_w[q, kw],   rel_h[q,kh] = q·Rh[qh-kh+S-1], rel_w likewise
+//   s[q,k] = scale * q.k + rel_h[q, kh] + rel_w[q, kw],   rel_h[q,kh] = q.Rh[qh-kh+S-1], rel_w likewise
 //
-// (rel-pos resize is an identity for SAM: 2*max(q,k)-1 == table length).
+// (rel-pos resize is an identity for SAM: 2*max(q,k)-1 == table length; scale = head_dim^-0.5).
 //
-// Layout/mapping (one wave = 32 queries, all MFMAs v_mfma_f32_32x32x16_bf16):
-//   S^T = K · Q^T  : A = K rows from LDS (XOR-swizzled), B = Q^T fragments kept in registers
-//                    -> every lane owns ONE query (col) and 16 keys (rows) per 32x32 tile
-//   O^T = V^T · P^T: A = V^T from LDS (padded rows, ds_read_b64), B = P^T taken straight from the
-//                    S^T accumulator registers (bf16-packed, k order permuted to match)
-//   so softmax statistics, the rel-pos terms and the O rescale are all per-lane (plus one
-//   lane^32 exchange) and nothing crosses lanes through LDS in the main loop.
-// rel_h / rel_w tables for the wave's queries are themselves MFMA products P^T = R · Q^T staged
-// once through LDS.
-//
-// Global layers (S=64, T=4096): 4 waves (128 queries = 2 image rows) per workgroup, 64-key tiles
-// (= one key image row, so rel_h is one scalar per lane per tile and rel_w is a fixed register set),
-// register-staged double-buffered K/V tiles.
-// Windowed layers (S=14, T=196): 7 waves (224 queries) per (window, head), the whole window's K/V
-// (padded to 256 keys, masked) resident in LDS.
+// One kernel template for both layer kinds, both head sizes (64: vit-b/l, 80: vit-h) and both 16-bit
+// element types (bf16; fp16 for BASELINE configs[4]):
+//   * 8 waves x 32 queries per workgroup; v_mfma_f32_32x32x16_{bf16,f16} throughout.
+//   * S^T = K . Q^T (operand-swapped): every lane owns ONE query (column) and 16 keys per 32x32 block, so
+//     softmax statistics, the rel-pos terms and the O rescale are per lane (+ one lane^32 exchange).
+//   * K / V stream global -> LDS with global_load_lds into a 3-deep ring of 64-key tiles (counted vmcnt +
+//     raw barrier). The first 64 head dims: K in a ds_read_b128 XOR-swizzled image, V row-major read
+//     transposed with ds_read_b64_tr_b16 (its image swaps 64-B halves on rows 2,3 mod 4: conflict-free).
+//     Head dim 80 adds a 16-dim tail image of K and V per tile (32-B rows, 4-B DMA granules, every wave
+//     issuing the same number of DMA ops): one more q.k step and a third 32-row O^T block whose rows
+//     80..95 read a zero block.
+//   * O^T = V^T . P^T takes P^T straight from the S^T accumulator registers (k order permuted to match).
+//   * Softmax in base 2: p = exp2(acc * scale*log2e + bias*log2e - m).
+// Global layers (side 64, T = 4096): 256 queries (4 image rows) per workgroup, 64 tiles of 64 keys (= one key
+// image row each, so rel_h is one LDS scalar per lane per tile and rel_w is the MFMA accumulator init).
+// Windowed layers (side 14, T = 196): two 4-wave workgroups per (window, head), keys in 16-column slots
+// (224 slots, 3.5 tiles; padding masked through the rel_w accumulator init), rel_w / rel_h per lane in
+// registers.
 #include "common.h"
 #include "../../include/octsam.h"
 
 namespace {
 
-constexpr float kScale = 0.125f;  // 64^-0.5, exact in bf16
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ int ksw(int r, int c) {  // K image [rows][64] bf16, 16-B chunk swizzle
-  return r * 64 + ((c ^ ((r >> 1) & 7)) << 3);
-}
+template <typename E> struct ET;
+template <> struct ET<bf16> {
+  typedef bf16x8 v8;
+  typedef bf16x4 v4;
+  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct ET<f16> {
+  typedef f16x8 v8;
+  typedef f16x4 v4;
+  static __device__ __forceinline__ f32x16 mma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
 
-__device__ __forceinline__ bf16x8 scale8(bf16x8 v) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = (bf16)((float)v[i] * kScale);
-  return v;
-}
+constexpr int NW = 8, THR = NW * 64, NBUF = 3;
+constexpr float L2E = 1.4426950408889634f;
 
-__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[base + j];
-  return r;
-}
+template <int HD> struct Geo {
+  static_assert(HD == 64 || HD == 80, "head_dim 64 or 80");
+  static constexpr int NKS = HD / 16;         // q.k steps of 16 dims
+  static constexpr int NTD = (HD + 31) / 32;  // 32-row blocks of O^T
+  static constexpr bool TAIL = HD > 64;       // the 16-dim tail images
+  static constexpr int K_OFF = 0, V_OFF = 8192, KT_OFF = 16384, VT_OFF = 16384 + 2048;
+  static constexpr int TILE = TAIL ? 16384 + 4096 : 16384;
+  static constexpr int OPS = TAIL ? 4 : 2;    // DMA ops per 8-row group per tile
+};
 
 // Row index (within a 32x32 tile) held in accumulator register r by lane half h.
 __device__ __forceinline__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-// P^T = R_ext · Qs^T for the wave's 32 queries; writes 8 * P^T (undo the 1/8 in Qs) to
-// prel[j * 33 + ql] for j in [0, 32*NJT) (rows >= 2S-1 are zero).
-template <int NJT>
-__device__ __forceinline__ void relpos_table(const float* __restrict__ R, int nrows, const bf16x8 (&qf)[4],
-                                             float* prel, int lane) {
-  const int h = lane >> 5, l32 = lane & 31;
-#pragma unroll
-  for (int t = 0; t < NJT; ++t) {
-    f32x16 acc = (f32x16)0.0f;
-    const int j = t * 32 + l32;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 a;
-      if (j < nrows) {
-        const float* rp = R + j * 64 + 16 * s + 8 * h;
-        float4 x0 = *(const float4*)rp, x1 = *(const float4*)(rp + 4);
-        a[0] = (bf16)x0.x; a[1] = (bf16)x0.y; a[2] = (bf16)x0.z; a[3] = (bf16)x0.w;
-        a[4] = (bf16)x1.x; a[5] = (bf16)x1.y; a[6] = (bf16)x1.z; a[7] = (bf16)x1.w;
-      } else {
-        a = (bf16x8)(bf16)0.0f;
-      }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) prel[(t * 32 + acc_row(r, h)) * 33 + l32] = acc[r] * 8.0f;
-  }
-}
-
-// ------------------------------------------------------------------------------------ global
-constexpr int G_NW = 4, G_THR = G_NW * 64;
-constexpr int VT_LD = 68;  // V^T row stride (bf16): 64 keys + 4 pad -> conflict-free ds_read_b64
-
-struct GSmem {
-  bf16 k[2][64 * 64];
-  bf16 vt[2][64 * VT_LD];
-  float prel[G_NW][128 * 33];
-};
-
-__global__ __launch_bounds__(G_THR) void vit_attn_global_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                                const float* __restrict__ Rh,
-                                                                const float* __restrict__ Rw, int heads) {
-  constexpr int S = 64, T = 4096;
-  __shared__ __attribute__((aligned(16))) GSmem sm;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int head = blockIdx.y, seq = blockIdx.z;
-  const int D = heads * 64, ld = 3 * D;
-  const bf16* base = qkv + (long long)seq * T * ld;
-  const int q = blockIdx.x * (G_NW * 32) + wave * 32 + l32;
-  const int qh = q >> 6, qw = q & 63;
-
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h));
-
-  // rel_w: fixed for the whole key loop (key tile = one key image row, kw = row index in tile)
-  float* prel = sm.prel[wave];
-  relpos_table<4>(Rw, 2 * S - 1, qf, prel, lane);
-  __syncthreads();
-  float relw[2][16];
-#pragma unroll
-  for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int kw = 32 * t2 + acc_row(r, h);
-      relw[t2][r] = prel[(qw - kw + S - 1) * 33 + l32];
-    }
-  __syncthreads();
-  relpos_table<4>(Rh, 2 * S - 1, qf, prel, lane);  // rel_h read per tile below
-
-  // K/V tile staging: 64 keys x 64 d, 512 16-B chunks of each, 2 per thread.
-  const bf16* kbase = base + D + head * 64;
-  const bf16* vbase = base + 2 * D + head * 64;
-  bf16x8 kreg[2], vreg[2];
-  auto gload = [&](int tile) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int ci = tid + i * G_THR;
-      int key = ci >> 3, c = ci & 7;
-      long long off = (long long)(tile * 64 + key) * ld + c * 8;
-      kreg[i] = *(const bf16x8*)(kbase + off);
-      vreg[i] = *(const bf16x8*)(vbase + off);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int ci = tid + i * G_THR;
-      int key = ci >> 3, c = ci & 7;
-      *(bf16x8*)(sm.k[buf] + ksw(key, c)) = kreg[i];
-      bf16* vt = sm.vt[buf];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vt[(c * 8 + e) * VT_LD + key] = vreg[i][e];
-    }
-  };
-
-  f32x16 acc_o[2];
-  acc_o[0] = (f32x16)0.0f;
-  acc_o[1] = (f32x16)0.0f;
-  float m_run = -INFINITY, l_run = 0.0f;
-
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  constexpr int NT = T / 64;
-  for (int tile = 0; tile < NT; ++tile) {
-    const int buf = tile & 1;
-    if (tile + 1 < NT) gload(tile + 1);
-    const bf16* sk = sm.k[buf];
-    const bf16* svt = sm.vt[buf];
-    f32x16 sacc[2];
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-      sacc[t2] = (f32x16)0.0f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 a = *(const bf16x8*)(sk + ksw(t2 * 32 + l32, 2 * s + h));
-        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
-      }
-    }
-    // tile = key image row kh
-    const float relh = prel[(qh - tile + S - 1) * 33 + l32];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = sacc[t2][r] + relw[t2][r] + relh;
-        sacc[t2][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = __expf(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.0f;
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __expf(sacc[t2][r] - m_new);
-        sacc[t2][r] = p;
-        ls += p;
-      }
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int td = 0; td < 2; ++td)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc_o[td][r] *= alpha;
-    // O^T += V^T · P^T over the 64 keys (4 k-steps of 16)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
-#pragma unroll
-      for (int td = 0; td < 2; ++td) {
-        const bf16* row = svt + (td * 32 + l32) * VT_LD + 16 * ks + 4 * h;
-        bf16x4 lo = *(const bf16x4*)row;
-        bf16x4 hi = *(const bf16x4*)(row + 8);
-        bf16x8 vf;
-        vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
-        vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
-        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[td], 0, 0, 0);
-      }
-    }
-    if (tile + 1 < NT) lstore(buf ^ 1);
-    __syncthreads();
-  }
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / l_tot;
-  bf16* orow = out + ((long long)seq * T + q) * D + head * 64;
-#pragma unroll
-  for (int td = 0; td < 2; ++td)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * g + e] * inv);
-      *(bf16x4*)(orow + td * 32 + 8 * g + 4 * h) = o;
-    }
-}
-
-// ------------------------------------------------------------------------------------ global, v2
-// 8 waves (256 queries = 4 image rows) per workgroup, two waves per SIMD so one wave's softmax overlaps
-// the other's MFMAs. K and V tiles (64 keys x 64 d) stream global -> LDS with global_load_lds into a
-// 3-deep ring (one instruction per wave per operand per tile, counted vmcnt + raw barrier). K keeps the
-// ds_read_b128 swizzle; V stays row-major and is read transposed with ds_read_b64_tr_b16 (its image
-// swaps 64-B halves on rows 2,3 mod 4 so the transposed reads are conflict-free). rel_w lives in
-// registers; rel_h as a [64 kh][32 q] fp32 table per wave. Softmax in base 2 (one FMA + exp per score).
-namespace g2 {
-constexpr int NW = 8, THR = NW * 64, NBUF = 3;
-constexpr int RELH_BYTES = NW * 64 * 32 * 4;       // 64 KiB
-constexpr int TILE_BYTES = 2 * 64 * 128;            // K + V, 16 KiB
-constexpr int SMEM = RELH_BYTES + NBUF * TILE_BYTES;  // 112 KiB
-constexpr int SCR_LD = 33;                          // rel_w scratch [96][33] per wave (overlaps the above)
-constexpr float L2E = 1.4426950408889634f;
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ int vsw(int r, int c) { return r * 128 + ((c ^ (((r >> 1) & 1) << 2)) << 4); }
 __device__ __forceinline__ int ksw_b(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
@@ -258,128 +80,229 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <int N> __device__ __forceinline__ void wait_vm();
+template <> __device__ __forceinline__ void wait_vm<0>() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <> __device__ __forceinline__ void wait_vm<2>() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+template <> __device__ __forceinline__ void wait_vm<4>() { asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
+template <> __device__ __forceinline__ void wait_vm<8>() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
 
+template <typename E>
+__device__ __forceinline__ typename ET<E>::v8 pack8(const f32x16& a, int base) {
+  typename ET<E>::v8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (E)a[base + j];
+  return r;
+}
 
-// 32 table rows j0 .. j0+31 of P^T = R · Qs^T (times 8: undo the 1/8 folded into Qs), rows >= nrows zero.
-__device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows, const bf16x8 (&qf)[4],
-                                            int lane) {
+// 32 table rows j0 .. j0+31 of P^T = R . Q^T for the lane's query (natural units), rows outside [0, nrows)
+// zero. R fp32 [nrows][HD], rounded to the element type like the q.k operands.
+template <int HD, typename E>
+__device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows,
+                                            const typename ET<E>::v8 (&qf)[Geo<HD>::NKS], int lane) {
   const int h = lane >> 5, j = j0 + (lane & 31);
   f32x16 acc = (f32x16)0.0f;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    bf16x8 a;
+  for (int s = 0; s < Geo<HD>::NKS; ++s) {
+    typename ET<E>::v8 a;
     if (j >= 0 && j < nrows) {
-      const float* rp = R + j * 64 + 16 * s + 8 * h;
-      float4 x0 = *(const float4*)rp, x1 = *(const float4*)(rp + 4);
-      a[0] = (bf16)x0.x; a[1] = (bf16)x0.y; a[2] = (bf16)x0.z; a[3] = (bf16)x0.w;
-      a[4] = (bf16)x1.x; a[5] = (bf16)x1.y; a[6] = (bf16)x1.z; a[7] = (bf16)x1.w;
+      const float* rp = R + j * HD + 16 * s + 8 * h;
+      const float4 x0 = *(const float4*)rp, x1 = *(const float4*)(rp + 4);
+      a[0] = (E)x0.x; a[1] = (E)x0.y; a[2] = (E)x0.z; a[3] = (E)x0.w;
+      a[4] = (E)x1.x; a[5] = (E)x1.y; a[6] = (E)x1.z; a[7] = (E)x1.w;
     } else {
-      a = (bf16x8)(bf16)0.0f;
+      a = (typename ET<E>::v8)(E)0.0f;
     }
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], acc, 0, 0, 0);
+    acc = ET<E>::mma(a, qf[s], acc);
   }
-  return acc * 8.0f;
+  return acc;
 }
 
-// K and V tile `tile` -> ring slot: 8 instructions of 1 KiB (8 rows x 128 B) per operand, one per wave
-__device__ __forceinline__ void load_tile(const bf16* kbase, const bf16* vbase, int ld, int tile, char* slot,
-                                          int wave, int lane) {
-  const int r = wave * 8 + (lane >> 3), sl = lane & 7;
-  const long long row = (long long)(tile * 64 + r) * ld;
-  const int ck = sl ^ ((r >> 1) & 7), cv = sl ^ (((r >> 1) & 1) << 2);
-  __builtin_amdgcn_global_load_lds((const void*)(kbase + row + ck * 8), (lds_ptr_t)(slot + wave * 1024), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((const void*)(vbase + row + cv * 8), (lds_ptr_t)(slot + 8192 + wave * 1024), 16,
-                                   0, 0);
+// Key slots key0 .. key0+63 -> ring slot by NWV waves, every wave the same number of ops: per 8-row group
+// 1 KiB (8 rows x 128 B) of each first-64-dim image, and for head dim 80 256 B (8 rows x 32 B) of each tail. Global layers: slot = key.
+// Windowed layers (WIN): slot = 16 kh + kw (key rows padded 14 -> 16 columns, 14 rows -> 16), padding slots
+// load the window's last key (their scores are masked).
+template <int HD, bool WIN, int NWV, typename E>
+__device__ __forceinline__ void load_tile(const E* kbase, const E* vbase, int ld, int key0, char* slot, int wave,
+                                          int lane) {
+  using G = Geo<HD>;
+#pragma unroll
+  for (int i = 0; i < 8 / NWV; ++i) {  // 8-row groups of this wave
+    const int grp = wave + NWV * i;
+    const int r = grp * 8 + (lane >> 3), sl = lane & 7;
+    int key = key0 + r;
+    if constexpr (WIN) key = min((key >> 4) * 14 + min(key & 15, 13), 195);
+    const long long row = (long long)key * ld;
+    const int ck = sl ^ ((r >> 1) & 7), cv = sl ^ (((r >> 1) & 1) << 2);
+    __builtin_amdgcn_global_load_lds((const void*)(kbase + row + ck * 8), (lds_ptr_t)(slot + G::K_OFF + grp * 1024),
+                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(vbase + row + cv * 8), (lds_ptr_t)(slot + G::V_OFF + grp * 1024),
+                                     16, 0, 0);
+    if constexpr (G::TAIL) {
+      __builtin_amdgcn_global_load_lds((const void*)(kbase + row + 64 + 2 * sl),
+                                       (lds_ptr_t)(slot + G::KT_OFF + grp * 256), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vbase + row + 64 + 2 * sl),
+                                       (lds_ptr_t)(slot + G::VT_OFF + grp * 256), 4, 0, 0);
+    }
+  }
 }
-}  // namespace g2
 
-__global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16* __restrict__ qkv,
-                                                                      bf16* __restrict__ out,
-                                                                      const float* __restrict__ Rh,
-                                                                      const float* __restrict__ Rw, int heads) {
-  using namespace g2;
+// S^T block t2 (keys 32 t2 .. 32 t2 + 31 of the tile) = K . Q^T + init
+template <int HD, typename E>
+__device__ __forceinline__ f32x16 qk_block(const char* slot, int t2, const typename ET<E>::v8 (&qf)[Geo<HD>::NKS],
+                                           f32x16 init, int l32, int h) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  f32x16 acc = init;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const V8 a = *(const V8*)(slot + G::K_OFF + ksw_b(t2 * 32 + l32, 2 * s + h));
+    acc = ET<E>::mma(a, qf[s], acc);
+  }
+  if constexpr (G::TAIL) {
+    const V8 a = *(const V8*)(slot + G::KT_OFF + (t2 * 32 + l32) * 32 + 16 * h);
+    acc = ET<E>::mma(a, qf[4], acc);
+  }
+  return acc;
+}
+
+// O^T += V^T . P^T over keys 16 ks .. 16 ks + 15 of the tile (P^T k-slot j of lane half hh is key
+// 16ks + 8(j>>2) + 4hh + (j&3)); the tail block's rows 80..95 read the zero block.
+template <int HD, typename E>
+__device__ __forceinline__ void pv_step(const char* slot, const char* zero, int ks, const typename ET<E>::v8& pf,
+                                        f32x16 (&acc_o)[Geo<HD>::NTD], int lane) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const char* sv = slot + G::V_OFF;
+  const int r0 = 16 * ks + 4 * (g >> 1) + qq;
+#pragma unroll
+  for (int td = 0; td < 2; ++td) {
+    const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
+    const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
+    const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    acc_o[td] = ET<E>::mma(__builtin_bit_cast(V8, v8), pf, acc_o[td]);
+  }
+  if constexpr (G::TAIL) {
+    const bool z = (g & 1) != 0;  // rows 80..95 of the third block
+    const char* a0 = z ? zero + 32 * qq + 8 * pp : slot + G::VT_OFF + r0 * 32 + 8 * pp;
+    const char* a1 = z ? zero + 32 * qq + 8 * pp : slot + G::VT_OFF + (r0 + 8) * 32 + 8 * pp;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+    const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    acc_o[2] = ET<E>::mma(__builtin_bit_cast(V8, v8), pf, acc_o[2]);
+  }
+}
+
+template <int HD, typename E>
+__device__ __forceinline__ void store_out(E* orow, const f32x16 (&acc_o)[Geo<HD>::NTD], float inv, int h) {
+  using V4 = typename ET<E>::v4;
+#pragma unroll
+  for (int td = 0; td < Geo<HD>::NTD; ++td)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      if (td * 32 + 8 * gg + 8 > HD) continue;  // compile-time: the tail block holds dims 64..79 only
+      V4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (E)(acc_o[td][4 * gg + e] * inv);
+      *(V4*)(orow + td * 32 + 8 * gg + 4 * h) = o;
+    }
+}
+
+template <int HD, typename E>
+__device__ __forceinline__ void load_q(const E* qrow, typename ET<E>::v8 (&qf)[Geo<HD>::NKS], int h) {
+#pragma unroll
+  for (int s = 0; s < Geo<HD>::NKS; ++s) qf[s] = *(const typename ET<E>::v8*)(qrow + 16 * s + 8 * h);
+}
+
+// ------------------------------------------------------------------------------------ global (side 64)
+constexpr int G_RELH = NW * 64 * 32 * 4;  // rel_h tables [64 kh][32 q] fp32 per wave: 64 KiB
+constexpr int G_SCR = 96 * 33;           // rel_w scratch [96][33] fp32 per wave (overlays tables + ring)
+template <int HD> constexpr int g_smem() { return G_RELH + NBUF * Geo<HD>::TILE + 128; }
+
+template <int HD, typename E>
+__global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+                                                                 const float* __restrict__ Rh,
+                                                                 const float* __restrict__ Rw, int heads, float scale) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
   constexpr int S = 64, T = 4096, NT = T / 64;
+  static_assert(NW * G_SCR * 4 <= G_RELH + NBUF * G::TILE, "rel_w scratch must fit");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int head = blockIdx.y, seq = blockIdx.z;
-  const int D = heads * 64, ld = 3 * D;
-  const bf16* base = qkv + (long long)seq * T * ld;
+  const int D = heads * HD, ld = 3 * D;
+  const E* base = qkv + (long long)seq * T * ld;
   const int q = blockIdx.x * (NW * 32) + wave * 32 + l32;
   const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
-  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);  // static priority: the SIMD's two waves drift apart
+  const float c1 = scale * L2E;
+  if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the SIMD's 2 waves drift
 
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h));
+  V8 qf[G::NKS];
+  load_q<HD, E>(base + (long long)q * ld + head * HD, qf, h);
 
-  // rel_w (registers): rows j = qw - kw + 63 in [qw0, qw0 + 95) of the table, staged through scratch
-  float* scr = (float*)gsm + wave * (96 * SCR_LD);
+  // rel_w (registers): rows j = qw - kw + 63 in [qw0, qw0 + 95) of the table, staged through scratch, kept as
+  // the initial accumulator of the S^T chain in units of the raw q.k (divided by the scale)
+  float* scr = (float*)gsm + wave * G_SCR;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    const f32x16 t = rel_block(Rw, qw0 + 32 * b, 2 * S - 1, qf, lane);
+    const f32x16 t = rel_block<HD, E>(Rw, qw0 + 32 * b, 2 * S - 1, qf, lane);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * SCR_LD + l32] = t[r];
+    for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * 33 + l32] = t[r];
   }
   __syncthreads();
-  // rel_w in natural units, as the initial accumulator of the S^T chain (free: the MFMA's C operand)
+  const float inv_scale = 1.0f / scale;
   f32x16 relw[2];
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * SCR_LD + l32];
+    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * 33 + l32] * inv_scale;
   __syncthreads();
-  // rel_h table [kh][q]: row j = qh - kh + 63 -> block rows i = j - qh = 63 - kh
+  // rel_h table [kh][q] (log2 units): row j = qh - kh + 63 -> block rows i = j - qh = 63 - kh
   float* relh = (float*)gsm + wave * (64 * 32);
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    const f32x16 t = rel_block(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+    const f32x16 t = rel_block<HD, E>(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
   }
+  char* ring = gsm + G_RELH;
+  char* zero = ring + NBUF * G::TILE;
+  if (tid < 32) ((float*)zero)[tid] = 0.0f;
   __syncthreads();
 
-  const bf16* kbase = base + D + head * 64;
-  const bf16* vbase = base + 2 * D + head * 64;
-  char* ring = gsm + RELH_BYTES;
-  load_tile(kbase, vbase, ld, 0, ring, wave, lane);
-  load_tile(kbase, vbase, ld, 1, ring + TILE_BYTES, wave, lane);
+  const E* kbase = base + D + head * HD;
+  const E* vbase = base + 2 * D + head * HD;
+  load_tile<HD, false, NW, E>(kbase, vbase, ld, 0, ring, wave, lane);
+  load_tile<HD, false, NW, E>(kbase, vbase, ld, 64, ring + G::TILE, wave, lane);
 
-  f32x16 acc_o[2];
-  acc_o[0] = (f32x16)0.0f;
-  acc_o[1] = (f32x16)0.0f;
+  f32x16 acc_o[G::NTD];
+#pragma unroll
+  for (int td = 0; td < G::NTD; ++td) acc_o[td] = (f32x16)0.0f;
   float m_run = -INFINITY, l_run = 0.0f;  // base-2 running max / sum
-  // tr-read lane geometry (V^T operand): group g = lane >> 4, lane 4qq + pp of the group
-  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
 
   for (int tile = 0; tile < NT; ++tile) {
-    if (tile + 1 < NT) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tile + 1 < NT) wait_vm<G::OPS>();
+    else wait_vm<0>();
     raw_barrier();
-    if (tile + 2 < NT) load_tile(kbase, vbase, ld, tile + 2, ring + ((tile + 2) % NBUF) * TILE_BYTES, wave, lane);
-    const char* sk = ring + (tile % NBUF) * TILE_BYTES;
-    const char* sv = sk + 8192;
-    // S^T + rel_w (natural units): the chain starts from the rel_w registers
+    if (tile + 2 < NT)
+      load_tile<HD, false, NW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
+    const char* slot = ring + (tile % NBUF) * G::TILE;
     f32x16 sacc[2];
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 a = *(const bf16x8*)(sk + ksw_b(t2 * 32 + l32, 2 * s + h));
-        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], s == 0 ? relw[t2] : sacc[t2], 0, 0, 0);
-      }
-    }
+    for (int t2 = 0; t2 < 2; ++t2) sacc[t2] = qk_block<HD, E>(slot, t2, qf, relw[t2], l32, h);
     // tile = key image row kh: rel_h is one constant per lane (log2 units), so max and exponent take it
-    // once per tile: p = exp2(L2E * s + (rh - m)), one FMA + one exp per score
+    // once per tile: p = exp2(c1 * acc + (rh - m)), one FMA + one exp per score
     const float rh = relh[tile * 32 + l32];
-    // (no inline-asm v_max3 here: hipcc's hazard recognizer does not see an asm statement read the MFMA
-    // result registers, and an early read made the row max -- and the rounding -- nondeterministic)
     float mx = -INFINITY;
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sacc[t2][r], sacc[t2][r + 1]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, fmaf(mx, L2E, rh));
+    const float m_new = fmaxf(m_run, fmaf(mx, c1, rh));
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     const float c = rh - m_new;
@@ -388,369 +311,206 @@ __global__ __launch_bounds__(g2::THR, 2) void vit_attn_global2_kernel(const bf16
     for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], L2E, c));
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], c1, c));
         sacc[t2][r] = pv;
         ls += pv;
       }
     l_run = fmaf(l_run, alpha, ls);
     if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
 #pragma unroll
-      for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
+      for (int td = 0; td < G::NTD; ++td) acc_o[td] *= alpha;
     }
-    // O^T += V^T · P^T: P^T k-slot j of lane half hh is key 16ks + 8(j>>2) + 4hh + (j&3)
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
-#pragma unroll
-      for (int td = 0; td < 2; ++td) {
-        const int r0 = 16 * ks + 4 * (g >> 1) + qq;
-        const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
-        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
-        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);
-      }
-    }
+    for (int ks = 0; ks < 4; ++ks) pv_step<HD, E>(slot, zero, ks, pack8<E>(sacc[ks >> 1], 8 * (ks & 1)), acc_o, lane);
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / l_tot;
-  bf16* orow = out + ((long long)seq * T + q) * D + head * 64;
-#pragma unroll
-  for (int td = 0; td < 2; ++td)
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * gg + e] * inv);
-      *(bf16x4*)(orow + td * 32 + 8 * gg + 4 * h) = o;
-    }
+  store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
-// ------------------------------------------------------------------------------------ window
-constexpr int W_NW = 7, W_THR = W_NW * 64;
-constexpr int W_KEYS = 256;
-constexpr int WVT_LD = W_KEYS + 4;
+// ------------------------------------------------------------------------------------ window (side 14)
+// Keys are laid out in slots 16 kh + kw (kw < 14 real; 14 key rows -> slots 0..223, 3.5 tiles). A 32-slot
+// block holds key rows kh0 = 2 block and kh0 + 1, and accumulator register r of lane half h holds slot
+// (r & 3) + 8 (r >> 2) + 4 h, i.e. kw = (r & 3) + 8 ((r >> 2) & 1) + 4 h and kh = kh0 + (r >> 3). So the bias
+// rel_w[kw] + rel_h[kh] is an 8-entry per-lane vector (the accumulator init, -inf on the padding columns)
+// plus one constant per half block: one FMA per score, no per-score table selects.
+// Two workgroups of 4 waves per (window, head), queries 0..127 and 128..255 (valid < 196), so that two
+// workgroups share a CU and one's prologue (Q, first tiles, rel tables) overlaps the other's key loop.
+constexpr int WNW = 4, WTHR = WNW * 64;
+constexpr int W_SCR = 27 * 33;  // rel-table scratch [27 = 2*14-1 rows][33] fp32 per wave, in ring slot 2 (its
+                                // first tile load is issued after the tables are read)
+template <int HD> constexpr int w_smem() { return NBUF * Geo<HD>::TILE + 128; }
+static_assert(WNW * W_SCR * 4 <= Geo<64>::TILE, "rel-table scratch must fit in one ring slot");
+static_assert(w_smem<64>() <= 160 * 1024 / 3, "three windowed workgroups per CU at head_dim 64");
 
-struct WSmem {
-  bf16 k[W_KEYS * 64];
-  bf16 vt[64 * WVT_LD];
-  float prel[W_NW][2][32 * 33];
-};
-
-__global__ __launch_bounds__(W_THR) void vit_attn_window_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                                const float* __restrict__ Rh,
-                                                                const float* __restrict__ Rw, int heads) {
-  constexpr int S = 14, T = 196;
-  __shared__ __attribute__((aligned(16))) WSmem sm;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int head = blockIdx.y, win = blockIdx.x;
-  const int D = heads * 64, ld = 3 * D;
-  const bf16* base = qkv + (long long)win * T * ld;
-
-  // stage the whole window's K (row-major, swizzled) and V^T; keys >= 196 zero
-  for (int ci = tid; ci < W_KEYS * 8; ci += W_THR) {
-    int key = ci >> 3, c = ci & 7;
-    bf16x8 kv = (bf16x8)(bf16)0.0f, vv = (bf16x8)(bf16)0.0f;
-    if (key < T) {
-      kv = *(const bf16x8*)(base + (long long)key * ld + D + head * 64 + c * 8);
-      vv = *(const bf16x8*)(base + (long long)key * ld + 2 * D + head * 64 + c * 8);
-    }
-    *(bf16x8*)(sm.k + ksw(key, c)) = kv;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sm.vt[(c * 8 + e) * WVT_LD + key] = vv[e];
-  }
-
-  const int q = wave * 32 + l32;
-  const bool qvalid = q < T;
-  const int qh = qvalid ? q / S : 0, qw = qvalid ? q % S : 0;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = qvalid ? scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s + 8 * h))
-                   : (bf16x8)(bf16)0.0f;
-  relpos_table<1>(Rw, 2 * S - 1, qf, sm.prel[wave][0], lane);
-  relpos_table<1>(Rh, 2 * S - 1, qf, sm.prel[wave][1], lane);
-  __syncthreads();
-  float relw[S], relh[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    relw[i] = sm.prel[wave][0][(qw - i + S - 1) * 33 + l32];
-    relh[i] = sm.prel[wave][1][(qh - i + S - 1) * 33 + l32];
-  }
-
-  f32x16 acc_o[2];
-  acc_o[0] = (f32x16)0.0f;
-  acc_o[1] = (f32x16)0.0f;
-  float m_run = -INFINITY, l_run = 0.0f;
-#pragma unroll
-  for (int tile = 0; tile < W_KEYS / 64; ++tile) {
-    f32x16 sacc[2];
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-      sacc[t2] = (f32x16)0.0f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 a = *(const bf16x8*)(sm.k + ksw(tile * 64 + t2 * 32 + l32, 2 * s + h));
-        sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[t2], 0, 0, 0);
-      }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        // key index for lane half 0 and 1 (compile-time), selected by h
-        constexpr int dummy = 0;
-        (void)dummy;
-        const int k0 = tile * 64 + t2 * 32 + acc_row(r, 0);
-        const int k1 = k0 + 4;
-        float b0 = (k0 < T) ? relh[(k0 < T ? k0 : 0) / S] + relw[(k0 < T ? k0 : 0) % S] : -INFINITY;
-        float b1 = (k1 < T) ? relh[(k1 < T ? k1 : 0) / S] + relw[(k1 < T ? k1 : 0) % S] : -INFINITY;
-        float v = sacc[t2][r] + (h ? b1 : b0);
-        sacc[t2][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = __expf(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.0f;
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __expf(sacc[t2][r] - m_new);
-        sacc[t2][r] = p;
-        ls += p;
-      }
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int td = 0; td < 2; ++td)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc_o[td][r] *= alpha;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
-#pragma unroll
-      for (int td = 0; td < 2; ++td) {
-        const bf16* row = sm.vt + (td * 32 + l32) * WVT_LD + tile * 64 + 16 * ks + 4 * h;
-        bf16x4 lo = *(const bf16x4*)row;
-        bf16x4 hi = *(const bf16x4*)(row + 8);
-        bf16x8 vf;
-        vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
-        vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
-        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, acc_o[td], 0, 0, 0);
-      }
-    }
-  }
-  if (!qvalid) return;
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / l_tot;
-  bf16* orow = out + ((long long)win * T + q) * D + head * 64;
-#pragma unroll
-  for (int td = 0; td < 2; ++td)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * g + e] * inv);
-      *(bf16x4*)(orow + td * 32 + 8 * g + 4 * h) = o;
-    }
-}
-
-// ------------------------------------------------------------------------------------ window, v2
-// Same mapping as vit_attn_window_kernel (7 waves x 32 queries, the window's 196 keys padded to 256 and
-// masked, rel_w / rel_h from MFMA tables), with 64 KiB of LDS instead of 124 so that two workgroups share a
-// CU: K keeps the swizzled row image; V stays row-major (LDS image of global2's tr-read swizzle) and is
-// read transposed with ds_read_b64_tr_b16; the per-wave rel-pos tables are staged one after the other
-// through a scratch that overlays the V image before V is written. Key blocks that hold only padding
-// (keys 224..255: the second half of the last 64-key tile) are skipped.
-namespace w2 {
-constexpr int NW = 7, THR = NW * 64, KEYS = 256;
-constexpr int K_BYTES = KEYS * 128, V_BYTES = KEYS * 128;
-constexpr int SMEM = K_BYTES + V_BYTES;  // 64 KiB
-static_assert(NW * 32 * 33 * 4 <= V_BYTES, "rel-pos scratch must fit in the V image");
-}  // namespace w2
-
-__global__ __launch_bounds__(w2::THR, 2) void vit_attn_window2_kernel(const bf16* __restrict__ qkv,
-                                                                      bf16* __restrict__ out,
-                                                                      const float* __restrict__ Rh,
-                                                                      const float* __restrict__ Rw, int heads) {
-  using namespace g2;
-  constexpr int S = 14, T = 196;
+template <int HD, typename E>
+__global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+                                                              const float* __restrict__ Rh,
+                                                              const float* __restrict__ Rw, int heads, float scale) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  constexpr int S = 14, T = 196, NT = 4;  // 224 key slots in 4 tiles (the last one half used)
   extern __shared__ __attribute__((aligned(16))) char wsm[];
-  char* kimg = wsm;
-  char* vimg = wsm + w2::K_BYTES;
+  char* ring = wsm;
+  float* scr = (float*)(wsm + 2 * G::TILE) + (threadIdx.x >> 6) * W_SCR;
+  char* zero = wsm + NBUF * G::TILE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int head = blockIdx.y, win = blockIdx.x;
-  const int D = heads * 64, ld = 3 * D;
-  const bf16* base = qkv + (long long)win * T * ld;
-
-  // K rows (swizzled [256][64] image; keys >= 196 zero)
-  for (int ci = tid; ci < w2::KEYS * 8; ci += w2::THR) {
-    const int key = ci >> 3, c = ci & 7;
-    bf16x8 kv = (bf16x8)(bf16)0.0f;
-    if (key < T) kv = *(const bf16x8*)(base + (long long)key * ld + D + head * 64 + c * 8);
-    *(bf16x8*)(kimg + 2 * ksw(key, c)) = kv;
-  }
-  const int q = wave * 32 + l32;
+  // block x = (head, query half) fastest: the 2*heads workgroups of a window read the same qkv rows together
+  const int head = blockIdx.x >> 1, win = blockIdx.y;
+  const int D = heads * HD, ld = 3 * D;
+  const E* base = qkv + (long long)win * T * ld;
+  const int q = (blockIdx.x & 1) * (WNW * 32) + wave * 32 + l32;
   const bool qvalid = q < T;
-  const int qh = qvalid ? q / S : 0, qw = qvalid ? q % S : 0;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4)
-    qf[s4] = qvalid ? scale8(*(const bf16x8*)(base + (long long)q * ld + head * 64 + 16 * s4 + 8 * h))
-                    : (bf16x8)(bf16)0.0f;
-  // rel_w then rel_h through this wave's scratch (inside the V image; LDS ops of one wave run in order)
-  float* scr = (float*)vimg + wave * (32 * 33);
-  float relw[S], relh[S];
-  relpos_table<1>(Rw, 2 * S - 1, qf, scr, lane);
-#pragma unroll
-  for (int i = 0; i < S; ++i) relw[i] = scr[(qw - i + S - 1) * 33 + l32];
-  relpos_table<1>(Rh, 2 * S - 1, qf, scr, lane);
-#pragma unroll
-  for (int i = 0; i < S; ++i) relh[i] = scr[(qh - i + S - 1) * 33 + l32];
-  __syncthreads();  // every wave is done with its scratch: the V image may be written
-  for (int ci = tid; ci < w2::KEYS * 8; ci += w2::THR) {
-    const int key = ci >> 3, c = ci & 7;
-    bf16x8 vv = (bf16x8)(bf16)0.0f;
-    if (key < T) vv = *(const bf16x8*)(base + (long long)key * ld + 2 * D + head * 64 + c * 8);
-    *(bf16x8*)(vimg + vsw(key, c)) = vv;
-  }
-  __syncthreads();
+  const int qc = qvalid ? q : T - 1;
+  const int qh = qc / S, qw = qc % S;
+  const float c1 = scale * L2E;
 
-  f32x16 acc_o[2];
-  acc_o[0] = (f32x16)0.0f;
-  acc_o[1] = (f32x16)0.0f;
-  float m_run = -INFINITY, l_run = 0.0f;
-  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  V8 qf[G::NKS];
+  load_q<HD, E>(base + (long long)qc * ld + head * HD, qf, h);
+  const E* kbase = base + D + head * HD;
+  const E* vbase = base + 2 * D + head * HD;
+  load_tile<HD, true, WNW, E>(kbase, vbase, ld, 0, ring, wave, lane);
+  load_tile<HD, true, WNW, E>(kbase, vbase, ld, 64, ring + G::TILE, wave, lane);
+
+  // rel_w for this lane half's 8 kw columns (units of the raw q.k: divided by the scale) and rel_h for the 14
+  // key rows (log2 units), through this wave's scratch: table row j = q - i + 13
+  f32x16 init;
+  float relh[S];
+  {
+    const f32x16 t = rel_block<HD, E>(Rw, 0, 2 * S - 1, qf, lane);
 #pragma unroll
-  for (int tile = 0; tile < w2::KEYS / 64; ++tile) {
+    for (int r = 0; r < 16; ++r)
+      if (acc_row(r, h) < 2 * S - 1) scr[acc_row(r, h) * 33 + l32] = t[r];
+    const float inv_scale = 1.0f / scale;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int kw = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = kw < S ? scr[(qw - (kw < S ? kw : 0) + S - 1) * 33 + l32] * inv_scale : -INFINITY;
+      init[r] = v;
+      init[r + 8] = v;
+    }
+  }
+  {
+    const f32x16 t = rel_block<HD, E>(Rh, 0, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (acc_row(r, h) < 2 * S - 1) scr[acc_row(r, h) * 33 + l32] = t[r];
+#pragma unroll
+    for (int i = 0; i < S; ++i) relh[i] = scr[(qh - i + S - 1) * 33 + l32] * L2E;
+  }
+  if (tid < 32) ((float*)zero)[tid] = 0.0f;
+
+  f32x16 acc_o[G::NTD];
+#pragma unroll
+  for (int td = 0; td < G::NTD; ++td) acc_o[td] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+#pragma unroll
+  for (int tile = 0; tile < NT; ++tile) {
+    if (tile + 1 < NT) wait_vm<G::OPS * 8 / WNW>();
+    else wait_vm<0>();
+    raw_barrier();
+    if (tile + 2 < NT)
+      load_tile<HD, true, WNW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
+    const char* slot = ring + (tile % NBUF) * G::TILE;
     constexpr int dummy = 0;
     (void)dummy;
-    const int nb = tile == 3 ? 1 : 2;  // 32-key blocks holding a real key (keys < 224)
+    const int nb = tile == NT - 1 ? 1 : 2;  // 32-slot blocks holding keys (slots < 224)
     f32x16 sacc[2];
+    float mh[4];  // raw max per half block (registers 0-7: key row kh0, 8-15: kh0 + 1)
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
-      sacc[t2] = (f32x16)0.0f;
-      if (t2 < nb) {
+      if (t2 >= nb) continue;
+      sacc[t2] = qk_block<HD, E>(slot, t2, qf, init, l32, h);
+      float a = -INFINITY, b = -INFINITY;
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          bf16x8 a = *(const bf16x8*)(kimg + 2 * ksw(tile * 64 + t2 * 32 + l32, 2 * s4 + h));
-          sacc[t2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s4], sacc[t2], 0, 0, 0);
-        }
+      for (int r = 0; r < 8; r += 2) {
+        a = fmaxf(a, fmaxf(sacc[t2][r], sacc[t2][r + 1]));
+        b = fmaxf(b, fmaxf(sacc[t2][r + 8], sacc[t2][r + 9]));
       }
+      mh[2 * t2] = a;
+      mh[2 * t2 + 1] = b;
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int k0 = tile * 64 + t2 * 32 + acc_row(r, 0);
-        const int k1 = k0 + 4;
-        float b0 = (k0 < T) ? relh[(k0 < T ? k0 : 0) / S] + relw[(k0 < T ? k0 : 0) % S] : -INFINITY;
-        float b1 = (k1 < T) ? relh[(k1 < T ? k1 : 0) / S] + relw[(k1 < T ? k1 : 0) % S] : -INFINITY;
-        float v = sacc[t2][r] + (h ? b1 : b0);
-        sacc[t2][r] = v;
-        mx = fmaxf(mx, v);
-      }
+    for (int k = 0; k < 2 * nb; ++k) mx = fmaxf(mx, fmaf(mh[k], c1, relh[4 * tile + k]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = __expf(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     float ls = 0.0f;
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
+    for (int t2 = 0; t2 < 2; ++t2) {
+      if (t2 >= nb) continue;
+      const float c0 = relh[4 * tile + 2 * t2] - m_new, cc1 = relh[4 * tile + 2 * t2 + 1] - m_new;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = __expf(sacc[t2][r] - m_new);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], c1, r < 8 ? c0 : cc1));
         sacc[t2][r] = pv;
         ls += pv;
       }
-    l_run = l_run * alpha + ls;
+    }
+    l_run = fmaf(l_run, alpha, ls);
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
 #pragma unroll
-    for (int td = 0; td < 2; ++td) acc_o[td] *= alpha;
-    // O^T += V^T P^T over the tile's real 16-key steps (the last tile: keys 192..207 only)
-    const char* sv = vimg + tile * 64 * 128;
+      for (int td = 0; td < G::NTD; ++td) acc_o[td] *= alpha;
+    }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      if (tile == 3 && ks > 0) break;
-      const bf16x8 pf = pack8(sacc[ks >> 1], 8 * (ks & 1));
-#pragma unroll
-      for (int td = 0; td < 2; ++td) {
-        const int r0 = 16 * ks + 4 * (g >> 1) + qq;
-        const int ch = 4 * td + 2 * (g & 1) + (pp >> 1);
-        const char* a0 = sv + vsw(r0, ch) + 8 * (pp & 1);
-        const char* a1 = sv + vsw(r0 + 8, ch) + 8 * (pp & 1);
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        const s16x8 v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc_o[td] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, v8), pf, acc_o[td], 0, 0, 0);
-      }
+      if (ks >= 2 * nb) break;
+      pv_step<HD, E>(slot, zero, ks, pack8<E>(sacc[ks >> 1], 8 * (ks & 1)), acc_o, lane);
     }
   }
   if (!qvalid) return;
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / l_tot;
-  bf16* orow = out + ((long long)win * T + q) * D + head * 64;
-#pragma unroll
-  for (int td = 0; td < 2; ++td)
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (bf16)(acc_o[td][4 * gg + e] * inv);
-      *(bf16x4*)(orow + td * 32 + 8 * gg + 4 * h) = o;
+  store_out<HD, E>(out + ((long long)win * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
+}
+
+template <int HD, typename E>
+int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nseq, int side, int heads,
+           hipStream_t s) {
+  const float scale = 1.0f / sqrtf((float)HD);
+  if (side == 64) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)vit_attn_global_kernel<HD, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                g_smem<HD>());
+      attr = true;
     }
+    hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(4096 / (NW * 32), heads, nseq), dim3(THR), g_smem<HD>(),
+                       s, (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)vit_attn_window_kernel<HD, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                w_smem<HD>());
+      attr = true;
+    }
+    hipLaunchKernelGGL((vit_attn_window_kernel<HD, E>), dim3(2 * heads, nseq, 1), dim3(WTHR), w_smem<HD>(), s,
+                       (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+  }
+  return 0;
 }
 
 }  // namespace
 
-static int g_attn_v2 = 1;
-extern "C" void octsam_attention_set_variant(int32_t v) { g_attn_v2 = v; }
-
 extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w,
-                                    int32_t nseq, int32_t side, int32_t heads, int32_t head_dim, void* stream) {
-  OCTSAM_CHECK_ARG(qkv && out && rel_pos_h && rel_pos_w && nseq > 0 && heads > 0,
+                                    int32_t nseq, int32_t side, int32_t heads, int32_t head_dim, int32_t fp16,
+                                    void* stream) {
+  OCTSAM_CHECK_ARG(qkv && out && rel_pos_h && rel_pos_w && nseq > 0 && heads > 0 && nseq <= 65535,
                    "octsam_vit_attention: bad args");
-  OCTSAM_CHECK_ARG(head_dim == 64, "octsam_vit_attention: head_dim must be 64 (got %d)", head_dim);
+  OCTSAM_CHECK_ARG(head_dim == 64 || head_dim == 80, "octsam_vit_attention: head_dim must be 64 or 80 (got %d)",
+                   head_dim);
+  OCTSAM_CHECK_ARG(side == 64 || side == 14, "octsam_vit_attention: side must be 64 (global) or 14 (window), got %d",
+                   side);
+  OCTSAM_CHECK_ARG(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)rel_pos_h & 15) == 0 &&
+                       ((uintptr_t)rel_pos_w & 15) == 0,
+                   "octsam_vit_attention: operands must be 16-B aligned");
   hipStream_t s = (hipStream_t)stream;
-  if (side == 64 && g_attn_v2) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)vit_attn_global2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                g2::SMEM);
-      attr = true;
-    }
-    dim3 grid(4096 / (g2::NW * 32), heads, nseq);
-    hipLaunchKernelGGL(vit_attn_global2_kernel, grid, dim3(g2::THR), g2::SMEM, s, (const bf16*)qkv, (bf16*)out,
-                       rel_pos_h, rel_pos_w, heads);
-  } else if (side == 64) {
-    dim3 grid(4096 / (G_NW * 32), heads, nseq);
-    hipLaunchKernelGGL(vit_attn_global_kernel, grid, dim3(G_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
-                       rel_pos_w, heads);
-  } else if (side == 14 && g_attn_v2 == 2) {  // (64 KiB variant; VGPR-bound to one workgroup per CU like v1)
-    static bool wattr = false;
-    if (!wattr) {
-      (void)hipFuncSetAttribute((const void*)vit_attn_window2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                w2::SMEM);
-      wattr = true;
-    }
-    dim3 grid(nseq, heads, 1);
-    hipLaunchKernelGGL(vit_attn_window2_kernel, grid, dim3(w2::THR), w2::SMEM, s, (const bf16*)qkv, (bf16*)out,
-                       rel_pos_h, rel_pos_w, heads);
-  } else if (side == 14) {
-    dim3 grid(nseq, heads, 1);
-    hipLaunchKernelGGL(vit_attn_window_kernel, grid, dim3(W_THR), 0, s, (const bf16*)qkv, (bf16*)out, rel_pos_h,
-                       rel_pos_w, heads);
-  } else {
-    octsam::set_error("octsam_vit_attention: side must be 64 (global) or 14 (window), got %d", side);
-    return 1;
-  }
+  if (head_dim == 64)
+    fp16 ? launch<64, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s)
+         : launch<64, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s);
+  else
+    fp16 ? launch<80, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s)
+         : launch<80, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s);
   OCTSAM_LAUNCH_CHECK("octsam_vit_attention");
   return 0;
 }

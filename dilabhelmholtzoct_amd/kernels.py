@@ -130,27 +130,18 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
 
 def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor, rel_pos_w: torch.Tensor, *,
                   nseq: int, side: int, heads: int) -> torch.Tensor:
-    """Fused SAM ViT attention with decomposed rel-pos bias; see octsam_vit_attention."""
+    """Fused SAM ViT attention with decomposed rel-pos bias; see octsam_vit_attention. head_dim from the
+    rel-pos tables (64 or 80), element type from qkv (bf16 or fp16)."""
     _require_cuda(qkv, out, rel_pos_h, rel_pos_w)
-    if qkv.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
-        raise ValueError("vit_attention expects bf16 qkv/out")
-    if qkv.numel() != nseq * side * side * 3 * heads * 64:
-        raise ValueError("qkv shape does not match nseq/side/heads")
+    if qkv.dtype not in (torch.bfloat16, torch.float16) or out.dtype != qkv.dtype:
+        raise ValueError("vit_attention expects bf16 or fp16 qkv / out of the same type")
+    hd = rel_pos_h.shape[-1]
+    if qkv.numel() != nseq * side * side * 3 * heads * hd or out.numel() != nseq * side * side * heads * hd:
+        raise ValueError("qkv / out shape does not match nseq / side / heads / head_dim")
     rh = rel_pos_h.float().contiguous()  # (named, so a converted copy outlives the launch)
     rw = rel_pos_w.float().contiguous()
-    _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rh), ptr(rw), nseq, side, heads, 64)
-    return out
-
-
-def _f32(t):
-    return int(t.dtype == torch.float32)
-
-
-def axpby(a, b, out, *, alpha=1.0, beta=1.0, b_period=0, out2_f32=None, n=None):
-    """out = alpha*a + beta*b (b broadcast with period b_period); a or b may be None."""
-    n = out.numel() if n is None else n
-    _lib.call("octsam_axpby", ptr(a), _f32(a) if a is not None else 0, ptr(b), _f32(b) if b is not None else 0,
-              b_period, alpha, beta, ptr(out), _f32(out), ptr(out2_f32), n)
+    _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rh), ptr(rw), nseq, side, heads, hd,
+              int(qkv.dtype == torch.float16))
     return out
 
 

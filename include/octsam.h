@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 7
+#define OCTSAM_ABI_VERSION 8
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -125,15 +125,14 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
 
 /* ---------------------------------------------------------------- ViT attention
  * Replaces SamVisionAttention.forward + get_decomposed_rel_pos (hf:modeling_sam.py:729-882).
- * qkv: bf16 [nseq, side*side, 3*heads*64] (the qkv Linear output, column = part*D + head*64 + d);
- * out: bf16 [nseq, side*side, heads*64]; rel_pos_h/w: fp32 [2*side-1, 64].
- * side = 64 (global layers, nseq = batch) or 14 (windowed layers, nseq = batch * 25 windows).
- * softmax(q k^T / 8 + rel_h + rel_w) v with fp32 statistics; the T x T bias is never materialised. */
-/* select the global-attention kernel: 1 (default) = 8-wave LDS-DMA kernel with transposed V reads,
-   0 = 4-wave register-staged kernel (A/B testing) */
-void octsam_attention_set_variant(int32_t v);
+ * qkv: [nseq, side*side, 3*heads*head_dim] 16-bit (the qkv Linear output, column = part*D + head*head_dim + d);
+ * out: [nseq, side*side, heads*head_dim], same type; rel_pos_h/w: fp32 [2*side-1, head_dim].
+ * side = 64 (global layers, nseq = batch) or 14 (windowed layers, nseq = batch * 25 windows);
+ * head_dim = 64 (vit-b / vit-l) or 80 (vit-h); fp16 = 1: IEEE half operands, else bf16.
+ * softmax(q k^T / sqrt(head_dim) + rel_h + rel_w) v with fp32 statistics; the T x T bias is never
+ * materialised. 16-B aligned operands. */
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
-                         int32_t side, int32_t heads, int32_t head_dim, void* stream);
+                         int32_t side, int32_t heads, int32_t head_dim, int32_t fp16, void* stream);
 
 /* ---------------------------------------------------------------- element-wise / reductions / prompts */
 /* out[i] = alpha*a[i] + beta*b[b_period ? i % b_period : i]  (a or b may be NULL = 0); out2_f32 optional copy.

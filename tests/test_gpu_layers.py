@@ -81,56 +81,61 @@ def test_layernorm_gather_rows(cuda):
     assert torch.all(y[1] == 0) and torch.all(y[4] == 0)
 
 
-def _ref_attention(qkv, Rh, Rw, nseq, side, heads):
+def _ref_attention(qkv, Rh, Rw, nseq, side, heads, hd=64):
     """HF SamVisionAttention math (eager path) in fp32."""
     T = side * side
-    qkv = qkv.float().reshape(nseq, T, 3, heads, 64).permute(2, 0, 3, 1, 4).reshape(3, nseq * heads, T, 64)
+    qkv = qkv.float().reshape(nseq, T, 3, heads, hd).permute(2, 0, 3, 1, 4).reshape(3, nseq * heads, T, hd)
     q, k, v = qkv.unbind(0)
-    attn = (q * 0.125) @ k.transpose(-2, -1)
+    attn = (q * hd ** -0.5) @ k.transpose(-2, -1)
     idx = (torch.arange(side)[:, None] - torch.arange(side)[None, :] + side - 1).to(q.device)
-    Rh_ = Rh.float()[idx]  # [side, side, 64]
+    Rh_ = Rh.float()[idx]  # [side, side, hd]
     Rw_ = Rw.float()[idx]
-    rq = q.reshape(-1, side, side, 64)
+    rq = q.reshape(-1, side, side, hd)
     rel_h = torch.einsum("bhwc,hkc->bhwk", rq, Rh_)
     rel_w = torch.einsum("bhwc,wkc->bhwk", rq, Rw_)
     bias = (rel_h[:, :, :, :, None] + rel_w[:, :, :, None, :]).reshape(-1, T, T)
     attn = torch.softmax(attn + bias, dim=-1)
-    o = (attn @ v).reshape(nseq, heads, side, side, 64).permute(0, 2, 3, 1, 4).reshape(nseq, T, heads * 64)
+    o = (attn @ v).reshape(nseq, heads, side, side, hd).permute(0, 2, 3, 1, 4).reshape(nseq, T, heads * hd)
     return o
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hd", [64, 80])
 @pytest.mark.parametrize("side,nseq,heads", [(14, 6, 3), (64, 2, 2)])
-def test_vit_attention(cuda, side, nseq, heads):
+def test_vit_attention(cuda, side, nseq, heads, hd, dtype):
+    """Global (side 64) and windowed (side 14) attention, head_dim 64 (vit-b/l) and 80 (vit-h), bf16 and fp16
+    operands, vs fp32 attention on the same rounded inputs (rel-pos tables rounded like the kernel's)."""
     from dilabhelmholtzoct_amd import kernels
-    g = torch.Generator().manual_seed(side)
+    g = torch.Generator().manual_seed(side + hd)
     T = side * side
-    qkv = torch.randn(nseq, T, 3 * heads * 64, generator=g).to(cuda, torch.bfloat16)
-    Rh = (0.3 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
-    Rw = (0.3 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
-    # the kernel computes rel-pos from bf16 tables; feed the reference the same rounding
-    Rh_b, Rw_b = Rh.to(torch.bfloat16).float(), Rw.to(torch.bfloat16).float()
-    out = torch.empty(nseq, T, heads * 64, device=cuda, dtype=torch.bfloat16)
+    qkv = torch.randn(nseq, T, 3 * heads * hd, generator=g).to(cuda, dtype)
+    Rh = (0.3 * torch.randn(2 * side - 1, hd, generator=g)).to(cuda)
+    Rw = (0.3 * torch.randn(2 * side - 1, hd, generator=g)).to(cuda)
+    Rh_b, Rw_b = Rh.to(dtype).float(), Rw.to(dtype).float()
+    out = torch.empty(nseq, T, heads * hd, device=cuda, dtype=dtype)
     kernels.vit_attention(qkv, out, Rh, Rw, nseq=nseq, side=side, heads=heads)
-    ref = _ref_attention(qkv, Rh_b, Rw_b, nseq, side, heads)
+    ref = _ref_attention(qkv, Rh_b, Rw_b, nseq, side, heads, hd)
     err = (out.float() - ref).abs().max().item()
-    assert err < 2e-2, err
+    assert err < (2e-2 if dtype == torch.bfloat16 else 4e-3), err
 
 
+@pytest.mark.parametrize("hd", [64, 80])
 @pytest.mark.parametrize("side,nseq", [(14, 64), (64, 8)])
-def test_vit_attention_deterministic(cuda, side, nseq):
+def test_vit_attention_deterministic(cuda, side, nseq, hd):
     """Windowed (side 14) and global (side 64) attention at the encoder's shapes: repeated launches give
     identical bits (graph replay must reproduce eager steps exactly; an early read of an MFMA result
     register once made the global kernel's row max, and so its rounding, vary run to run)."""
     from dilabhelmholtzoct_amd import kernels
     g = torch.Generator().manual_seed(side + nseq)
     T = side * side
-    qkv = (0.5 * torch.randn(nseq * T, 3 * 768, generator=g)).to(cuda, torch.bfloat16)
-    Rh = (0.1 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
-    Rw = (0.1 * torch.randn(2 * side - 1, 64, generator=g)).to(cuda)
+    heads = 768 // 64 if hd == 64 else 16
+    qkv = (0.5 * torch.randn(nseq * T, 3 * heads * hd, generator=g)).to(cuda, torch.bfloat16)
+    Rh = (0.1 * torch.randn(2 * side - 1, hd, generator=g)).to(cuda)
+    Rw = (0.1 * torch.randn(2 * side - 1, hd, generator=g)).to(cuda)
     outs = []
     for _ in range(3):
-        o = torch.empty(nseq * T, 768, device=cuda, dtype=torch.bfloat16)
-        kernels.vit_attention(qkv, o, Rh, Rw, nseq=nseq, side=side, heads=12)
+        o = torch.empty(nseq * T, heads * hd, device=cuda, dtype=torch.bfloat16)
+        kernels.vit_attention(qkv, o, Rh, Rw, nseq=nseq, side=side, heads=heads)
         outs.append(o)
     assert all(torch.equal(outs[0], o) for o in outs[1:])
 
