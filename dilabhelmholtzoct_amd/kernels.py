@@ -145,6 +145,18 @@ def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor,
     return out
 
 
+def _f32(t):
+    return int(t.dtype == torch.float32)
+
+
+def axpby(a, b, out, *, alpha=1.0, beta=1.0, b_period=0, out2_f32=None, n=None):
+    """out = alpha*a + beta*b (b broadcast with period b_period); a or b may be None."""
+    n = out.numel() if n is None else n
+    _lib.call("octsam_axpby", ptr(a), _f32(a) if a is not None else 0, ptr(b), _f32(b) if b is not None else 0,
+              b_period, alpha, beta, ptr(out), _f32(out), ptr(out2_f32), n)
+    return out
+
+
 def patchify_bf16(px, out):
     """pixel_values fp32 [B, 3, 1024, 1024] -> patch rows bf16 [B*4096, 768] (k = c, ky, kx)."""
     _require_cuda(px, out)
