@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--model", default="facebook/sam-vit-base")
     p.add_argument("--prompt", default="bboxes", choices=["bboxes", "points", "both"])
     p.add_argument("--top", type=int, default=1)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                   help="16-bit operand type of the frozen encoder (fp16: BASELINE configs[4]); the decoder is bf16")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle step (rank 0, N=1)")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--val", type=int, default=8, help="val images for the Dice readout (0 = skip)")
@@ -179,9 +181,11 @@ def make_batch(args, rank, device, processor):
 
 def workload_name(args) -> str:
     short = args.model.rsplit("/", 1)[-1]
-    desc = f"{short}, --prompt={args.prompt}, --top={bool(args.top)}, bf16, batch {args.batch}/GPU"
+    desc = f"{short}, --prompt={args.prompt}, --top={bool(args.top)}, {args.dtype}, batch {args.batch}/GPU"
     if short == "sam-vit-base" and args.prompt == "bboxes":
         return f"BASELINE configs[{2 if args.top else 1}]: {desc}"
+    if short == "sam-vit-huge" and args.prompt == "both" and args.top and args.dtype == "fp16":
+        return f"BASELINE configs[4] (per-GPU slice of batch 64 over 8 GPUs): {desc}"
     if args.prompt == "both":
         return f"BASELINE configs[4] prompt mode (box + point per component) on {desc}"
     if short == "sam-vit-large" and args.prompt == "points" and args.top:
@@ -408,6 +412,8 @@ def main():
     N = int(batch["gt_u8"].shape[1])
 
     model = SamModel.from_pretrained(args.model, seed=0).to(device)
+    if args.dtype == "fp16":
+        model.set_encoder_dtype(torch.float16)
     step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager)
 
     def barrier():
@@ -547,7 +553,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 4), "unit": "imgs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.dtype == "bf16" else "fp16 encoder, bf16 decoder (fp32 master weights)",
             "data": f"synthetic OCT-like 496x512 label maps -> 1024x1024 processed images, {N} "
                     f"{'point' if args.prompt == 'points' else 'box'} prompts/image (batch max), random-init "
                     f"weights (seed 0)",

@@ -43,6 +43,7 @@ _SIGNATURES = {
     "octsam_abi_version": (c_int32, []),
     "octsam_last_error": (ctypes.c_char_p, []),
     "octsam_gemm": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
+    "octsam_gemm_f16": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
     "octsam_gemm_set_fast_path": (None, [c_int32]),
     "octsam_gemm_last_path": (c_int32, []),
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
@@ -65,7 +66,9 @@ _SIGNATURES = {
                                        c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
     "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "octsam_cast_f16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "octsam_patchify_bf16": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "octsam_patchify_f16": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cc_label": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
                                   c_void_p]),
     "octsam_cc_assign": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p,

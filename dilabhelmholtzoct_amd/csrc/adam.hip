@@ -26,9 +26,10 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   if (pb) pb[i] = (bf16)pv;
 }
 
-__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+template <typename E>
+__global__ void cast16_kernel(const float* __restrict__ x, E* __restrict__ y, long long n) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = (bf16)x[i];
+  if (i < n) y[i] = (E)x[i];
 }
 }  // namespace
 
@@ -47,8 +48,16 @@ extern "C" int octsam_adam(float* params, const float* grads, float* exp_avg, fl
 
 extern "C" int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream) {
   OCTSAM_CHECK_ARG(x && y && n > 0, "octsam_cast_bf16: bad args");
-  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(cast16_kernel<bf16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
                      (bf16*)y, n);
   OCTSAM_LAUNCH_CHECK("octsam_cast_bf16");
+  return 0;
+}
+
+extern "C" int octsam_cast_f16(const float* x, void* y, int64_t n, void* stream) {
+  OCTSAM_CHECK_ARG(x && y && n > 0, "octsam_cast_f16: bad args");
+  hipLaunchKernelGGL(cast16_kernel<_Float16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     x, (_Float16*)y, n);
+  OCTSAM_LAUNCH_CHECK("octsam_cast_f16");
   return 0;
 }

@@ -1,4 +1,4 @@
-// MFMA bf16 GEMM for gfx950 with fused epilogues and implicit-GEMM operand loaders.
+// MFMA e16 GEMM for gfx950 with fused epilogues and implicit-GEMM operand loaders.
 //
 //   C[b][m][n] = epi( alpha * sum_k A[b][m][k] * B[b][n][k] )          (fp32 accumulate)
 //
@@ -7,7 +7,7 @@
 //   1  transposed A[k*lda + m]                     (dY^T for weight gradients)
 //   2  patch16    A from fp32 NCHW pixels          (SamPatchEmbeddings conv 16x16/s16 as im2col,
 //                                                   hf modeling_sam.py:116-129)
-//   3  conv3x3    A from bf16 NHWC 64x64 map, k = (ky*3+kx)*C + c, zero padding 1
+//   3  conv3x3    A from e16 NHWC 64x64 map, k = (ky*3+kx)*C + c, zero padding 1
 //                                                  (SamVisionNeck.conv2, modeling_sam.py:985-992)
 //   4  row-major plus a row-periodic addend A2[(m % a2_rows)*lda + k]   (keys + key_pe,
 //                                                  SamTwoWayAttentionBlock, modeling_sam.py:327-343)
@@ -20,12 +20,61 @@
 // pre-activation store; optional output row remap (window unpartition: drop padded tokens).
 //
 // Tiling: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 via 2x2 v_mfma_f32_32x32x16_bf16.
-// LDS image [row][64] bf16 with the 16-byte chunk index XOR-swizzled by ((row>>1)&7) so that the
+// LDS image [row][64] e16 with the 16-byte chunk index XOR-swizzled by ((row>>1)&7) so that the
 // ds_read_b128 lane groups of the 32x32x16 fragment reads are conflict-free.
 // Register-staged double buffer, one barrier per K-step; XCD-aware block remap so that the tiles
 // of one A row-panel run on one XCD (shared L2).
 #include "common.h"
 #include "../../include/octsam.h"
+
+// 16-bit operand type of this build: bf16 (octsam_gemm) or IEEE half (built again with OCTSAM_GEMM_F16:
+// octsam_gemm_f16, the fp16 encoder of BASELINE configs[4]). The two MFMA shapes and the epilogue's
+// 16-bit <-> fp32 conversions are the only type-dependent operations; data movement is byte-agnostic.
+#ifdef OCTSAM_GEMM_F16
+typedef _Float16 e16;
+typedef _Float16 e16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 e16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 e16x2 __attribute__((ext_vector_type(2)));
+#define OCTSAM_GEMM_ENTRY octsam_gemm_f16
+#else
+typedef bf16 e16;
+typedef bf16x8 e16x8;
+typedef bf16x4 e16x4;
+typedef bf16x2 e16x2;
+#define OCTSAM_GEMM_ENTRY octsam_gemm
+#endif
+
+namespace {
+__device__ __forceinline__ f32x16 mma32(e16x8 a, e16x8 b, f32x16 c, int, int, int) {
+#ifdef OCTSAM_GEMM_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+__device__ __forceinline__ f32x4 mma16(e16x8 a, e16x8 b, f32x4 c, int, int, int) {
+#ifdef OCTSAM_GEMM_F16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+// low / high 16-bit element of a packed pair as fp32
+__device__ __forceinline__ float lo16f(uint32_t r) {
+#ifdef OCTSAM_GEMM_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(r & 0xffffu));
+#else
+  return __builtin_bit_cast(float, r << 16);
+#endif
+}
+__device__ __forceinline__ float hi16f(uint32_t r) {
+#ifdef OCTSAM_GEMM_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(r >> 16));
+#else
+  return __builtin_bit_cast(float, r & 0xffff0000u);
+#endif
+}
+}  // namespace
 
 namespace {
 
@@ -59,86 +108,86 @@ __device__ __forceinline__ long long remap(int row, int blk, int rep) {
   return blk > 0 ? (long long)(row / (blk * rep)) * blk + row % blk : (long long)row;
 }
 
-__device__ __forceinline__ int lds_idx(int r, int c) {  // bf16 element index in a [rows][64] image
+__device__ __forceinline__ int lds_idx(int r, int c) {  // e16 element index in a [rows][64] image
   return r * BK + ((c ^ ((r >> 1) & 7)) << 3);
 }
 
-__device__ __forceinline__ bf16x8 cvt8(const float4 a, const float4 b) {
-  bf16x8 r;
-  r[0] = (bf16)a.x; r[1] = (bf16)a.y; r[2] = (bf16)a.z; r[3] = (bf16)a.w;
-  r[4] = (bf16)b.x; r[5] = (bf16)b.y; r[6] = (bf16)b.z; r[7] = (bf16)b.w;
+__device__ __forceinline__ e16x8 cvt8(const float4 a, const float4 b) {
+  e16x8 r;
+  r[0] = (e16)a.x; r[1] = (e16)a.y; r[2] = (e16)a.z; r[3] = (e16)a.w;
+  r[4] = (e16)b.x; r[5] = (e16)b.y; r[6] = (e16)b.z; r[7] = (e16)b.w;
   return r;
 }
 
-// Stage: each thread holds R/32 chunks of 8 bf16 for the operand tile (R rows x 64 k).
+// Stage: each thread holds R/32 chunks of 8 e16 for the operand tile (R rows x 64 k).
 template <int MODE, int R = 128>
 struct Loader {
   static constexpr int NC = R / 32;  // chunks per thread
   static constexpr int RC = R / 8;   // 8-row chunks per k row (transposed modes)
-  bf16x8 v[NC];
+  e16x8 v[NC];
 
   __device__ __forceinline__ void load(const GemmK& p, const void* base, const void* add, int period,
                                        long long ld, int rows, int row0, int k0, int tid, int blk, int rep,
                                        int kcap) {
     if constexpr (MODE == 4) {
-      const bf16* src = (const bf16*)base;
-      const bf16* ad = (const bf16*)add;
+      const e16* src = (const e16*)base;
+      const e16* ad = (const e16*)add;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
         if (gr < rows && gk < p.K) {
-          bf16x8 x = *(const bf16x8*)(src + remap(gr, blk, rep) * ld + gk);
-          bf16x8 y = *(const bf16x8*)(ad + (long long)(gr % period) * ld + gk);
+          e16x8 x = *(const e16x8*)(src + remap(gr, blk, rep) * ld + gk);
+          e16x8 y = *(const e16x8*)(ad + (long long)(gr % period) * ld + gk);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
+          for (int e = 0; e < 8; ++e) x[e] = (e16)((float)x[e] + (float)y[e]);
           v[i] = x;
         } else {
-          v[i] = (bf16x8)(bf16)0.0f;
+          v[i] = (e16x8)(e16)0.0f;
         }
       }
     } else if constexpr (MODE == 5) {  // B mode 2: transposed plus k-periodic addend
-      const bf16* src = (const bf16*)base;
-      const bf16* ad = (const bf16*)add;
+      const e16* src = (const e16*)base;
+      const e16* ad = (const e16*)add;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int k = ci / RC, rc = ci % RC;
         int gr = row0 + rc * 8, gk = k0 + k;
         if (gr < rows && gk < p.K) {
-          bf16x8 x = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
-          bf16x8 y = *(const bf16x8*)(ad + (long long)(gk % period) * ld + gr);
+          e16x8 x = *(const e16x8*)(src + remap(gk, blk, rep) * ld + gr);
+          e16x8 y = *(const e16x8*)(ad + (long long)(gk % period) * ld + gr);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] = (bf16)((float)x[e] + (float)y[e]);
+          for (int e = 0; e < 8; ++e) x[e] = (e16)((float)x[e] + (float)y[e]);
           v[i] = x;
         } else {
-          v[i] = (bf16x8)(bf16)0.0f;
+          v[i] = (e16x8)(e16)0.0f;
         }
       }
     } else if constexpr (MODE == 0) {
-      const bf16* src = (const bf16*)base;
+      const e16* src = (const e16*)base;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
         if (gr < rows && gk < p.K)
-          v[i] = *(const bf16x8*)(src + remap(gr, blk, rep) * ld + gk);
+          v[i] = *(const e16x8*)(src + remap(gr, blk, rep) * ld + gk);
         else
-          v[i] = (bf16x8)(bf16)0.0f;
+          v[i] = (e16x8)(e16)0.0f;
       }
     } else if constexpr (MODE == 1) {
-      const bf16* src = (const bf16*)base;
+      const e16* src = (const e16*)base;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int k = ci / RC, rc = ci % RC;
         int gr = row0 + rc * 8, gk = k0 + k;
         if (gr < rows && gk < kcap)
-          v[i] = *(const bf16x8*)(src + remap(gk, blk, rep) * ld + gr);
+          v[i] = *(const e16x8*)(src + remap(gk, blk, rep) * ld + gr);
         else
-          v[i] = (bf16x8)(bf16)0.0f;
+          v[i] = (e16x8)(e16)0.0f;
       }
     } else if constexpr (MODE == 2) {
       const float* px = (const float*)base;
@@ -155,31 +204,31 @@ struct Loader {
           float4 a1 = *(const float4*)(s + 4);
           v[i] = cvt8(a0, a1);
         } else {
-          v[i] = (bf16x8)(bf16)0.0f;
+          v[i] = (e16x8)(e16)0.0f;
         }
       }
-    } else {  // MODE 3: conv3x3 over NHWC 64x64 bf16
-      const bf16* src = (const bf16*)base;
+    } else {  // MODE 3: conv3x3 over NHWC 64x64 e16
+      const e16* src = (const e16*)base;
       const int C = p.conv_c;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
         int gr = row0 + r, gk = k0 + c * 8;
-        bf16x8 val = (bf16x8)(bf16)0.0f;
+        e16x8 val = (e16x8)(e16)0.0f;
         if (gr < rows && gk < p.K) {
           int b = gr >> 12, y = (gr >> 6) & 63, x = gr & 63;
           int tap = gk / C, ch = gk - tap * C;
           int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
           if (yy >= 0 && yy < 64 && xx >= 0 && xx < 64)
-            val = *(const bf16x8*)(src + (((long long)b * 64 + yy) * 64 + xx) * C + ch);
+            val = *(const e16x8*)(src + (((long long)b * 64 + yy) * 64 + xx) * C + ch);
         }
         v[i] = val;
       }
     }
   }
 
-  __device__ __forceinline__ void store(bf16* lds, int tid) {
+  __device__ __forceinline__ void store(e16* lds, int tid) {
     if constexpr (MODE == 1 || MODE == 5) {
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
@@ -196,7 +245,7 @@ struct Loader {
       for (int i = 0; i < NC; ++i) {
         int ci = tid + i * NTHR;
         int r = ci >> 3, c = ci & 7;
-        *(bf16x8*)(lds + lds_idx(r, c)) = v[i];
+        *(e16x8*)(lds + lds_idx(r, c)) = v[i];
       }
     }
   }
@@ -206,7 +255,7 @@ struct Loader {
 template <int AM, int BMODE, int T = 128>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
   constexpr int MB = T / 64;  // 32x32 MFMA blocks per wave and dimension
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (T + T) * BK];
+  __shared__ __attribute__((aligned(16))) e16 smem[2 * (T + T) * BK];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -246,8 +295,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
-    bf16* sa = smem + (kt & 1) * (T + T) * BK;
-    bf16* sb = sa + T * BK;
+    e16* sa = smem + (kt & 1) * (T + T) * BK;
+    e16* sb = sa + T * BK;
     const bool more = kt + 1 < nk;
     if (more) {
       la.load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, (kt + 1) * BK, tid, p.a_blk, p.a_rep, kcap);
@@ -256,19 +305,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const int ch = kk * 2 + (lane >> 5);
-      bf16x8 af[MB], bfr[MB];
+      e16x8 af[MB], bfr[MB];
 #pragma unroll
-      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(sa + lds_idx(wm * (T / 2) + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < MB; ++i) af[i] = *(const e16x8*)(sa + lds_idx(wm * (T / 2) + i * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int j = 0; j < MB; ++j) bfr[j] = *(const bf16x8*)(sb + lds_idx(wn * (T / 2) + j * 32 + (lane & 31), ch));
+      for (int j = 0; j < MB; ++j) bfr[j] = *(const e16x8*)(sb + lds_idx(wn * (T / 2) + j * 32 + (lane & 31), ch));
 #pragma unroll
       for (int i = 0; i < MB; ++i)
 #pragma unroll
         for (int j = 0; j < MB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      bf16* na = smem + ((kt + 1) & 1) * (T + T) * BK;
+      e16* na = smem + ((kt + 1) & 1) * (T + T) * BK;
       la.store(na, tid);
       lb.store(na + T * BK, tid);
     }
@@ -297,20 +346,20 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
         }
         const long long ci = (long long)om * p.ldc + n;
         float v = acc[i][j][r] * p.alpha;
-        if (p.beta != 0.0f) v += p.beta * (p.c_f32 ? ((float*)Cb)[ci] : (float)((bf16*)Cb)[ci]);
+        if (p.beta != 0.0f) v += p.beta * (p.c_f32 ? ((float*)Cb)[ci] : (float)((e16*)Cb)[ci]);
         v += bv;
         if (Pb) {
           if (p.pre_f32) ((float*)Pb)[ci] = v;
-          else ((bf16*)Pb)[ci] = (bf16)v;
+          else ((e16*)Pb)[ci] = (e16)v;
         }
         if (p.act == OCTSAM_ACT_RELU) v = fmaxf(v, 0.0f);
         else if (p.act == OCTSAM_ACT_GELU) v = gelu_erf(v);
         if (Rb) {
           const long long ri = remap(om, p.r_blk, p.r_rep) * p.ldr + n;
-          v += p.r_f32 ? ((const float*)Rb)[ri] : (float)((const bf16*)Rb)[ri];
+          v += p.r_f32 ? ((const float*)Rb)[ri] : (float)((const e16*)Rb)[ri];
         }
         if (p.c_f32) ((float*)Cb)[ci] = v;
-        else ((bf16*)Cb)[ci] = (bf16)v;
+        else ((e16*)Cb)[ci] = (e16)v;
       }
     }
   }
@@ -354,7 +403,7 @@ __device__ __forceinline__ int sw_off(int r, int c) {  // byte offset of 16-B ch
 }
 
 template <int BK>
-__device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long long ld, int rows, int row0, int k0,
+__device__ __forceinline__ void glds_tile(const e16* __restrict__ src, long long ld, int rows, int row0, int k0,
                                           char* lds, int nrows_tile, int wave, int lane) {
   constexpr int CPR = BK / 8;          // 16-B chunks per row
   constexpr int RPI = 64 / CPR;        // rows per wave-instruction (1 KiB)
@@ -368,7 +417,7 @@ __device__ __forceinline__ void glds_tile(const bf16* __restrict__ src, long lon
     else c = slot ^ ((r >> 2) & 3);
     int gr = row0 + r;
     gr = gr < rows ? gr : rows - 1;
-    const bf16* g = src + (long long)gr * ld + k0 + c * 8;
+    const e16* g = src + (long long)gr * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(lds + j * 1024), 16, 0, 0);
   }
 }
@@ -383,7 +432,7 @@ __device__ __forceinline__ int km_off(int r, int ch) { return r * 256 + ((ch ^ (
 __device__ uint4 g_zero16[4];  // 16 zero bytes: LDS-DMA source of k rows past the end of a K tail
 
 template <int TX>
-__device__ __forceinline__ void glds_tile_km(const bf16* __restrict__ src, long long ld, int xdim, int x0, int k0,
+__device__ __forceinline__ void glds_tile_km(const e16* __restrict__ src, long long ld, int xdim, int x0, int k0,
                                              char* lds, int wave, int lane, int kmax = 0x7fffffff) {
   constexpr int NINST = TX / 8;  // 64 rows * TX * 2 B / 1 KiB
 #pragma unroll
@@ -392,7 +441,7 @@ __device__ __forceinline__ void glds_tile_km(const bf16* __restrict__ src, long 
     const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
     int col = x0 + h * 128 + ch * 8;
     col = col < xdim ? col : xdim - 8;
-    const bf16* g = k0 + r < kmax ? src + (long long)(k0 + r) * ld + col : (const bf16*)g_zero16;
+    const e16* g = k0 + r < kmax ? src + (long long)(k0 + r) * ld + col : (const e16*)g_zero16;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(lds + h * 16384 + (j & 15) * 1024), 16, 0, 0);
   }
 }
@@ -401,7 +450,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // 32x32x16 MFMA operand (8 consecutive k of row xb + (lane & 31), k from kb + 8*(lane>>5)) from a k-major image
-__device__ __forceinline__ bf16x8 frag_km(const char* img, int xb, int kb, int lane) {
+__device__ __forceinline__ e16x8 frag_km(const char* img, int xb, int kb, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
   const int x = xb + 16 * (g & 1);
   const int h = x >> 7, c0 = (x & 127) >> 3;
@@ -411,28 +460,28 @@ __device__ __forceinline__ bf16x8 frag_km(const char* img, int xb, int kb, int l
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + km_off(r0 + 4, c0 + (pp >> 1))));
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
+  return __builtin_bit_cast(e16x8, v);
 }
 
 // Fast epilogue: adjacent lanes trade one value with a DPP quad swap so each lane owns two adjacent
 // columns of one row (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n) and writes them with one
-// 4-B (bf16x2) or 8-B (float2) store. Loads are hoisted ahead of the stores so a store never waits on an
-// earlier store's completion (vmcnt counts both): bias + row map first, then a bf16 residual for the whole
+// 4-B (e16x2) or 8-B (float2) store. Loads are hoisted ahead of the stores so a store never waits on an
+// earlier store's completion (vmcnt counts both): bias + row map first, then a e16 residual for the whole
 // wave tile; an fp32 residual or a beta*C read is loaded per 32-column group (one wait per group).
 // Requires N, ldc (and ldr) even and 4/8-B aligned C / R / C_pre (checked on the host).
 __device__ __forceinline__ float2 ld_pair(const void* base, long long idx, bool f32) {
   if (f32) return *(const float2*)((const float*)base + idx);
-  const uint32_t r = *(const uint32_t*)((const bf16*)base + idx);
-  return make_float2(__builtin_bit_cast(float, r << 16), __builtin_bit_cast(float, r & 0xffff0000u));
+  const uint32_t r = *(const uint32_t*)((const e16*)base + idx);
+  return make_float2(lo16f(r), hi16f(r));
 }
 __device__ __forceinline__ void st_pair(void* base, long long idx, bool f32, float lo, float hi) {
   if (f32) {
     *(float2*)((float*)base + idx) = make_float2(lo, hi);
   } else {
-    bf16x2 w;
-    w[0] = (bf16)lo;
-    w[1] = (bf16)hi;
-    *(bf16x2*)((bf16*)base + idx) = w;
+    e16x2 w;
+    w[0] = (e16)lo;
+    w[1] = (e16)hi;
+    *(e16x2*)((e16*)base + idx) = w;
   }
 }
 __device__ __forceinline__ float dpp_swap1(float x) {
@@ -474,7 +523,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
         for (int t = 0; t < 8; ++t) {
           const int o = om[i][t];
           rv[LATE ? 0 : i][LATE ? 0 : j][t] = (o >= 0 && c < p.N)
-                            ? *(const uint32_t*)((const bf16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
+                            ? *(const uint32_t*)((const e16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
         }
       }
   }
@@ -530,8 +579,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x16 (&acc)[NI][
             hi += lr[i][t].y;
           } else {
             const uint32_t r = rv[LATE ? 0 : i][LATE ? 0 : j][t];
-            lo += __builtin_bit_cast(float, r << 16);
-            hi += __builtin_bit_cast(float, r & 0xffff0000u);
+            lo += lo16f(r);
+            hi += hi16f(r);
           }
         }
         if (ok) st_pair(Cb, ci, p.c_f32, lo, hi);
@@ -576,10 +625,10 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
     tile_of(i, bz, r0, c0);
     char* st = gsm + (g % NS) * STAGE;
     const int kmax = p.k_total > 0 ? p.k_total - bz * p.K : 0x7fffffff;
-    if constexpr (AKM) glds_tile_km<BM_>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, wave, lane, kmax);
-    else glds_tile<BK>((const bf16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
-    if constexpr (BKM) glds_tile_km<BN_>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, wave, lane, kmax);
-    else glds_tile<BK>((const bf16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
+    if constexpr (AKM) glds_tile_km<BM_>((const e16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, wave, lane, kmax);
+    else glds_tile<BK>((const e16*)p.A + bz * p.sA, p.lda, p.M, r0, kt * BK, st, BM_, wave, lane);
+    if constexpr (BKM) glds_tile_km<BN_>((const e16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, wave, lane, kmax);
+    else glds_tile<BK>((const e16*)p.B + bz * p.sB, p.ldb, p.N, c0, kt * BK, st + A_BYTES, BN_, wave, lane);
   };
 
   f32x16 acc[2][NJ];
@@ -604,22 +653,22 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const int ch = kk * 2 + (lane >> 5);
-      bf16x8 af[2], bfr[NJ];
+      e16x8 af[2], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (AKM) af[i] = frag_km(sa, wm * 64 + i * 32, kk * 16, lane);
-        else af[i] = *(const bf16x8*)(sa + sw_off<BK>(wm * 64 + i * 32 + (lane & 31), ch));
+        else af[i] = *(const e16x8*)(sa + sw_off<BK>(wm * 64 + i * 32 + (lane & 31), ch));
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if constexpr (BKM) bfr[j] = frag_km(sb, wn * (BN_ / 2) + j * 32, kk * 16, lane);
-        else bfr[j] = *(const bf16x8*)(sb + sw_off<BK>(wn * (BN_ / 2) + j * 32 + (lane & 31), ch));
+        else bfr[j] = *(const e16x8*)(sb + sw_off<BK>(wn * (BN_ / 2) + j * 32 + (lane & 31), ch));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (g % nk == nk - 1) {
       int bz, r0, c0;
@@ -674,13 +723,13 @@ int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 // vmcnt before the first barrier of the phase preceding the read, raw s_barrier, and the two wave rows
 // run one barrier apart so one row's MFMAs overlap the other's LDS reads.
 namespace ph8 {
-constexpr int BUF = 65536;  // A [256][64] + B [256][64] bf16
+constexpr int BUF = 65536;  // A [256][64] + B [256][64] e16
 
 // region 0 A-lo, 1 A-hi, 2 B-n0, 3 B-n1: 128 rows x 128 B = 16 instructions of 8 rows, 2 per wave
-__device__ __forceinline__ void load_region(const GemmK& p, const bf16* A, const bf16* B, int region, int row0,
+__device__ __forceinline__ void load_region(const GemmK& p, const e16* A, const e16* B, int region, int row0,
                                             int col0, int k0, char* buf, int wave, int lane) {
   const bool isA = region < 2;
-  const bf16* src = isA ? A : B;
+  const e16* src = isA ? A : B;
   const long long ld = isA ? p.lda : p.ldb;
   const int lim = isA ? p.M : p.N, g0 = isA ? row0 : col0;
 #pragma unroll
@@ -692,13 +741,13 @@ __device__ __forceinline__ void load_region(const GemmK& p, const bf16* A, const
     const int c = slot ^ ((r >> 1) & 7);
     int gr = g0 + r;
     gr = gr < lim ? gr : lim - 1;
-    const bf16* g = src + (long long)gr * ld + k0 + c * 8;
+    const e16* g = src + (long long)gr * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(buf + (isA ? 0 : 32768) + rbase * 128), 16, 0, 0);
   }
 }
 
-__device__ __forceinline__ bf16x8 frag(const char* img, int row, int kc) {
-  return *(const bf16x8*)(img + sw_off<64>(row, kc));
+__device__ __forceinline__ e16x8 frag(const char* img, int row, int kc) {
+  return *(const e16x8*)(img + sw_off<64>(row, kc));
 }
 
 // lane: col n = lane & 15, rows 4*(lane>>4) + i. Pairs (i, i+1) of adjacent lanes are merged by a DPP
@@ -735,7 +784,7 @@ __device__ __forceinline__ void epilogue16(const GemmK& p, f32x4 (&acc)[8][4], i
         for (int t = 0; t < 2; ++t) {
           const int o = om[mi][t];
           rv[LATE ? 0 : mi][LATE ? 0 : ni][t] =
-              (o >= 0 && c < p.N) ? *(const uint32_t*)((const bf16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
+              (o >= 0 && c < p.N) ? *(const uint32_t*)((const e16*)Rb + remap(o, p.r_blk, p.r_rep) * p.ldr + c) : 0u;
         }
       }
   }
@@ -787,8 +836,8 @@ __device__ __forceinline__ void epilogue16(const GemmK& p, f32x4 (&acc)[8][4], i
             hi += lr[mi][t].y;
           } else {
             const uint32_t r = rv[LATE ? 0 : mi][LATE ? 0 : ni][t];
-            lo += __builtin_bit_cast(float, r << 16);
-            hi += __builtin_bit_cast(float, r & 0xffff0000u);
+            lo += lo16f(r);
+            hi += hi16f(r);
           }
         }
         if (ok) st_pair(Cb, ci, p.c_f32, lo, hi);
@@ -798,7 +847,7 @@ __device__ __forceinline__ void epilogue16(const GemmK& p, f32x4 (&acc)[8][4], i
 
 // LDS-staged epilogue: the fp32 tile goes through LDS in two 128-row passes ([128][256+4] fp32,
 // padded against bank conflicts) and every lane then finishes 8 consecutive columns of one row with
-// 16-B vector loads (bias, residual, beta*C) and 16-B (bf16) / 2x16-B (fp32) stores: full cache lines
+// 16-B vector loads (bias, residual, beta*C) and 16-B (e16) / 2x16-B (fp32) stores: full cache lines
 // instead of the MFMA layout's 32-B row segments. Requires N, ldc (ldr) % 8 == 0 and 16-B aligned
 // C / C_pre / R (host-checked).
 constexpr int EPI_LD = 260;
@@ -809,7 +858,7 @@ __device__ __forceinline__ void load8(const void* base, long long idx, bool f32,
     const float4 a = *(const float4*)((const float*)base + idx), b = *(const float4*)((const float*)base + idx + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   } else {
-    const bf16x8 a = *(const bf16x8*)((const bf16*)base + idx);
+    const e16x8 a = *(const e16x8*)((const e16*)base + idx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = (float)a[e];
   }
@@ -819,10 +868,10 @@ __device__ __forceinline__ void store8(void* base, long long idx, bool f32, cons
     *(float4*)((float*)base + idx) = make_float4(v[0], v[1], v[2], v[3]);
     *(float4*)((float*)base + idx + 4) = make_float4(v[4], v[5], v[6], v[7]);
   } else {
-    bf16x8 a;
+    e16x8 a;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = (bf16)v[e];
-    *(bf16x8*)((bf16*)base + idx) = a;
+    for (int e = 0; e < 8; ++e) a[e] = (e16)v[e];
+    *(e16x8*)((e16*)base + idx) = a;
   }
 }
 
@@ -888,7 +937,7 @@ __device__ __forceinline__ void epilogue_lds(const GemmK& p, f32x4 (&acc)[8][4],
 // Register epilogue for the operand-swapped MFMA: acc[mi][ni] holds the 16x16 block transposed, so lane
 // (q = lane>>4, r = lane&15) owns output row m = 16*mi + r and the 4 consecutive columns 16*ni + 4q .. +3.
 // One v_permlane16_swap per value between blocks (2p, 2p+1) gives every lane 8 consecutive columns of its
-// row, starting at 32p + 16*(q&1) + 8*(q>>1): 16-B bf16 (32-B fp32) stores, 64-B row runs per
+// row, starting at 32p + 16*(q&1) + 8*(q>>1): 16-B e16 (32-B fp32) stores, 64-B row runs per
 // instruction, no LDS round trip and no barrier (the next tile's loads can be in flight). Every input the
 // stores depend on (row map, bias, residual, beta*C) is loaded before the first store, so no load waits
 // behind a store (vmcnt counts both). Requires N, ldc (ldr) % 8 == 0 and 16-B aligned C / C_pre / R / bias.
@@ -967,7 +1016,7 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
       for (int pr = 0; pr < 2; ++pr) {
         const int n = col0 + 32 * pr + cofs;
         raw[mi][pr] = (om[mi] >= 0 && n < p.N)
-                          ? *(const u32x4*)((const bf16*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n)
+                          ? *(const u32x4*)((const e16*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n)
                           : (u32x4)0u;
       }
 #pragma unroll
@@ -977,8 +1026,8 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
         float res[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          res[2 * e] = __builtin_bit_cast(float, raw[mi][pr][e] << 16);
-          res[2 * e + 1] = __builtin_bit_cast(float, raw[mi][pr][e] & 0xffff0000u);
+          res[2 * e] = lo16f(raw[mi][pr][e]);
+          res[2 * e + 1] = hi16f(raw[mi][pr][e]);
         }
         finish(mi, pr, res);
       }
@@ -1025,8 +1074,8 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
   _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                                     \
   _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                                     \
     acc[(MH) * 4 + mi][(NH) * 2 + ni] =                                                                 \
-        TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(BF[ni][kb], af[mi][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0) \
-           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
+        TR ? mma16(BF[ni][kb], af[mi][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0) \
+           : mma16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
 
 // EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA)
@@ -1045,8 +1094,8 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   const int bz = bid / per_batch, rem = bid - bz * per_batch;
   const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
   const int row0 = tm * 256, col0 = tn * 256;
-  const bf16* A = (const bf16*)p.A + bz * p.sA;
-  const bf16* B = (const bf16*)p.B + bz * p.sB;
+  const e16* A = (const e16*)p.A + bz * p.sA;
+  const e16* B = (const e16*)p.B + bz * p.sB;
   const int nk = p.K / 64;
 
   f32x4 acc[8][4];
@@ -1054,7 +1103,7 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  e16x8 af[4][2], b0[2][2], b1[2][2];
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
 
   // prologue: K-tile 0 (A-lo, B-n0 | B-n1 | A-hi), K-tile 1 (A-lo, B-n0 | B-n1)
@@ -1167,8 +1216,8 @@ int launch_gemm8(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 // exact and the waits are relaxed by it, so the stores drain under that step's MFMAs.
 namespace ph8 {
 struct Cursor {  // the K-step a prefetch targets: tile i (this workgroup's i-th), K-tile kt
-  const bf16* A;
-  const bf16* B;
+  const e16* A;
+  const e16* B;
   int row0, col0, i, kt;
 };
 __device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, int stride, int per_batch) {
@@ -1176,8 +1225,8 @@ __device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, 
   const int bz = t / per_batch, rem = t - bz * per_batch;
   const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
   Cursor c;
-  c.A = (const bf16*)p.A + bz * p.sA;
-  c.B = (const bf16*)p.B + bz * p.sB;
+  c.A = (const e16*)p.A + bz * p.sA;
+  c.B = (const e16*)p.B + bz * p.sB;
   c.row0 = tm * 256;
   c.col0 = tn * 256;
   c.i = i;
@@ -1186,7 +1235,7 @@ __device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, 
 }
 template <int BASE>
 __device__ __forceinline__ void vm_wait(bool relax) {
-  // relax: the 16 store instructions of a full bf16 tile's epilogue sit above the loads this wait retires
+  // relax: the 16 store instructions of a full e16 tile's epilogue sit above the loads this wait retires
   (void)relax;
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE) : "memory");
 }
@@ -1209,7 +1258,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
   const int nk = p.K / 64;
   const int G = mycnt * nk;
   if (G == 0) return;
-  // only bf16-output epilogues without a pre-activation copy have the exact 16-store count the relaxed
+  // only e16-output epilogues without a pre-activation copy have the exact 16-store count the relaxed
   // waits assume; everything else waits for its stores (conservative)
   const bool relax_ok = !p.c_f32 && p.Cpre == nullptr && p.row_map == nullptr;
 
@@ -1218,7 +1267,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  e16x8 af[4][2], b0[2][2], b1[2][2];
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
 
   // prefetch cursors: c1 -> step g+1, c2 -> step g+2 (advanced once per step; divisions once per tile)
@@ -1409,6 +1458,7 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 static int g_use_glds = 1;
 static int g_small = 1;
 static thread_local int t_last_path = 0;
+#ifndef OCTSAM_GEMM_F16
 // enable: 0 = generic kernels only; 1 = default; 2..10 = fast-path variants (diagnostics); bit 8 (256)
 // disables the small-problem 64x64 path
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
@@ -1416,8 +1466,9 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_use_glds = enable & 255;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
+#endif
 
-extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
+extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   OCTSAM_CHECK_ARG(a != nullptr, "octsam_gemm: null args");
   OCTSAM_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0 && a->batch > 0, "octsam_gemm: bad sizes M=%d N=%d K=%d batch=%d",
                    a->M, a->N, a->K, a->batch);
@@ -1526,6 +1577,7 @@ extern "C" int octsam_gemm(const octsam_gemm_args* a, void* stream) {
   return 1;
 }
 
+#ifndef OCTSAM_GEMM_F16
 extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
                                     void* stream) {
   OCTSAM_CHECK_ARG(partials && out && n > 0 && splits > 0, "octsam_splitk_reduce: bad args");
@@ -1550,3 +1602,4 @@ extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n
   OCTSAM_LAUNCH_CHECK("octsam_splitk_reduce");
   return 0;
 }
+#endif  // OCTSAM_GEMM_F16

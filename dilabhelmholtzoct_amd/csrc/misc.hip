@@ -256,8 +256,9 @@ extern "C" int octsam_group_sum(const void* in, int64_t ld_in, int32_t cols, int
 // conv as a plain NT GEMM on the 8-phase kernel. One thread per 8 consecutive pixels of an image row:
 // 32-B coalesced reads, one 16-B store.
 namespace {
-__global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ px, bf16* __restrict__ out,
-                                                       long long n8) {
+template <typename E>
+__global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ px, E* __restrict__ out, long long n8) {
+  typedef E E8 __attribute__((ext_vector_type(8)));
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n8) return;
   const int x8 = (int)(i & 127), y = (int)((i >> 7) & 1023);
@@ -265,20 +266,30 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
   const int c = (int)(bc % 3);
   const long long b = bc / 3;
   const float4 a0 = *(const float4*)(px + i * 8), a1 = *(const float4*)(px + i * 8 + 4);
-  bf16x8 v;
-  v[0] = (bf16)a0.x; v[1] = (bf16)a0.y; v[2] = (bf16)a0.z; v[3] = (bf16)a0.w;
-  v[4] = (bf16)a1.x; v[5] = (bf16)a1.y; v[6] = (bf16)a1.z; v[7] = (bf16)a1.w;
+  E8 v;
+  v[0] = (E)a0.x; v[1] = (E)a0.y; v[2] = (E)a0.z; v[3] = (E)a0.w;
+  v[4] = (E)a1.x; v[5] = (E)a1.y; v[6] = (E)a1.z; v[7] = (E)a1.w;
   const long long row = b * 4096 + (y >> 4) * 64 + (x8 >> 1);
-  *(bf16x8*)(out + row * 768 + c * 256 + (y & 15) * 16 + (x8 & 1) * 8) = v;
+  *(E8*)(out + row * 768 + c * 256 + (y & 15) * 16 + (x8 & 1) * 8) = v;
 }
 }  // namespace
 
-extern "C" int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream) {
+static int patchify(const float* px, int32_t B, void* out, bool f16, void* stream) {
   OCTSAM_CHECK_ARG(px && out && B > 0 && ((uintptr_t)px & 15) == 0 && ((uintptr_t)out & 15) == 0,
-                   "octsam_patchify_bf16: bad args (16-B aligned operands required)");
+                   "octsam_patchify: bad args (16-B aligned operands required)");
   const long long n8 = (long long)B * 3 * 1024 * 128;
-  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, px,
-                     (bf16*)out, n8);
-  OCTSAM_LAUNCH_CHECK("octsam_patchify_bf16");
+  const dim3 grid((unsigned)((n8 + 255) / 256));
+  if (f16)
+    hipLaunchKernelGGL(patchify_kernel<_Float16>, grid, dim3(256), 0, (hipStream_t)stream, px, (_Float16*)out, n8);
+  else
+    hipLaunchKernelGGL(patchify_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, px, (bf16*)out, n8);
+  OCTSAM_LAUNCH_CHECK("octsam_patchify");
   return 0;
+}
+
+extern "C" int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream) {
+  return patchify(px, B, out, false, stream);
+}
+extern "C" int octsam_patchify_f16(const float* px, int32_t B, void* out, void* stream) {
+  return patchify(px, B, out, true, stream);
 }

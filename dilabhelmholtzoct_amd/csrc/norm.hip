@@ -63,21 +63,31 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, w);
 }
 
+__device__ __forceinline__ uint32_t pack2h(float a, float b) {  // IEEE half pair (the fp16 encoder)
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  h2 w;
+  w[0] = (_Float16)a;
+  w[1] = (_Float16)b;
+  return __builtin_bit_cast(uint32_t, w);
+}
+
+// ty: 1 = fp32, 2 = fp16, otherwise bf16
 template <int CW>
-__device__ __forceinline__ void stv(void* base, long long idx, bool f32, const float* v) {
-  if (f32) {
+__device__ __forceinline__ void stv(void* base, long long idx, int ty, const float* v) {
+  if (ty == 1) {
     float* p = (float*)base + idx;
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
     if constexpr (CW == 8) *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
   } else {
     bf16* p = (bf16*)base + idx;
+    auto pk = [&](float a, float b) { return ty == 2 ? pack2h(a, b) : pack2(a, b); };
     if constexpr (CW == 8) {
       u32x4 a;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] = pack2(v[2 * e], v[2 * e + 1]);
+      for (int e = 0; e < 4; ++e) a[e] = pk(v[2 * e], v[2 * e + 1]);
       *(u32x4*)p = a;
     } else {
-      *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      *(uint2*)p = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
     }
   }
 }
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       stv<CW>(y, row * D + CW * j + G * CW * c, y_f32, out + c * CW);
-      if (y2) stv<CW>(y2, row * D + CW * j + G * CW * c, true, out + c * CW);  // fp32 residual-stream copy
+      if (y2) stv<CW>(y2, row * D + CW * j + G * CW * c, 1, out + c * CW);  // fp32 residual-stream copy
     }
   }
 }

@@ -25,8 +25,15 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
          A2: torch.Tensor | None = None, B2: torch.Tensor | None = None, a2_rows: int = 0,
          b2_rows: int = 0, conv_c: int = 0, a_remap: tuple[int, int] = (0, 1),
          b_remap: tuple[int, int] = (0, 1), r_remap: tuple[int, int] = (0, 1), k_total: int = 0) -> torch.Tensor:
-    """C[b] = epi(alpha * A[b] @ B[b]^T); see octsam_gemm in include/octsam.h."""
+    """C[b] = epi(alpha * A[b] @ B[b]^T); see octsam_gemm in include/octsam.h. The 16-bit operand type (bf16 or
+    fp16: octsam_gemm_f16) is B's; every other 16-bit operand must match it."""
     _require_cuda(A, B, out, bias, residual, pre_out, row_map, A2, B2)
+    e16 = B.dtype
+    if e16 not in (torch.bfloat16, torch.float16):
+        raise ValueError(f"B must be bf16 or fp16, got {e16}")
+    for name, t in (("A", A), ("out", out), ("residual", residual), ("pre_out", pre_out), ("A2", A2), ("B2", B2)):
+        if t is not None and t.dtype not in (e16, torch.float32):
+            raise ValueError(f"{name} is {t.dtype}; the GEMM's 16-bit type is {e16}")
     if a_mode in (0, 4):
         lda = K if lda is None else lda
     elif a_mode == 1:
@@ -50,7 +57,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         pre_f32=int(pre_out is not None and pre_out.dtype == torch.float32),
         conv_c=conv_c, a2_rows=a2_rows, b2_rows=b2_rows, a_blk=a_remap[0], a_rep=a_remap[1],
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total)
-    _lib.call("octsam_gemm", ctypes.byref(args))
+    _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
 
 
@@ -96,8 +103,11 @@ def layernorm_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float,
     D = w.numel()
     if rows is None:
         rows = out.numel() // D
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("layernorm input must be fp32 or bf16")
+    yty = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2}[out.dtype]
     _lib.call("octsam_layernorm_fwd", ptr(x), int(x.dtype == torch.float32), ptr(src_rows), rows, D, ptr(w),
-              ptr(b), eps, ptr(out), int(out.dtype == torch.float32), ptr(out2_f32), act, ptr(mean), ptr(rstd))
+              ptr(b), eps, ptr(out), yty, ptr(out2_f32), act, ptr(mean), ptr(rstd))
     return out
 
 
@@ -158,14 +168,17 @@ def axpby(a, b, out, *, alpha=1.0, beta=1.0, b_period=0, out2_f32=None, n=None):
 
 
 def patchify_bf16(px, out):
-    """pixel_values fp32 [B, 3, 1024, 1024] -> patch rows bf16 [B*4096, 768] (k = c, ky, kx)."""
+    """pixel_values fp32 [B, 3, 1024, 1024] -> patch rows [B*4096, 768] (k = c, ky, kx), bf16 or fp16 (out's
+    type)."""
     _require_cuda(px, out)
-    _lib.call("octsam_patchify_bf16", ptr(px), px.shape[0], ptr(out))
+    _lib.call("octsam_patchify_f16" if out.dtype == torch.float16 else "octsam_patchify_bf16", ptr(px), px.shape[0],
+              ptr(out))
     return out
 
 
 def cast_bf16(x, out):
-    _lib.call("octsam_cast_bf16", ptr(x), ptr(out), x.numel())
+    """fp32 -> out's 16-bit type (bf16 or fp16)."""
+    _lib.call("octsam_cast_f16" if out.dtype == torch.float16 else "octsam_cast_bf16", ptr(x), ptr(out), x.numel())
     return out
 
 

@@ -92,15 +92,18 @@ class VisionEncoder(nn.Module):
         self.neck = VisionNeck(cfg)
         self._wcache: dict = {}
         self._maps: dict = {}
+        # 16-bit operand type of the encoder's MFMA work: bf16 (BASELINE configs[1..3]) or fp16 (configs[4]);
+        # the residual stream, LayerNorm statistics and accumulation stay fp32
+        self.compute_dtype = torch.bfloat16
 
-    # bf16 operand cache, refreshed whenever a parameter is modified in place or moved
+    # 16-bit operand cache, refreshed whenever a parameter is modified in place or moved
     def _w(self, key, p: torch.Tensor, fn=None):
         ent = self._wcache.get(key)
-        tag = (p._version, p.data_ptr(), p.device)
+        tag = (p._version, p.data_ptr(), p.device, self.compute_dtype)
         if ent is None or ent[0] != tag:
             t = p.detach()
             t = fn(t) if fn is not None else t
-            ent = (tag, t.to(torch.bfloat16).contiguous())
+            ent = (tag, t.to(self.compute_dtype).contiguous())
             self._wcache[key] = ent
         return ent[1]
 
@@ -146,6 +149,7 @@ class VisionEncoder(nn.Module):
         px = pixel_values.float().contiguous()
         B = px.shape[0]
         D = cfg.hidden_size
+        e16 = self.compute_dtype
         g = cfg.image_size // cfg.patch_size
         L = g * g
         M = B * L
@@ -153,13 +157,13 @@ class VisionEncoder(nn.Module):
         heads = cfg.num_attention_heads
         pe = self.patch_embed.projection
         x = torch.empty(M, D, device=dev, dtype=torch.float32)
-        patches = K.patchify_bf16(px, torch.empty(M, 3 * 256, device=dev, dtype=torch.bfloat16))
+        patches = K.patchify_bf16(px, torch.empty(M, 3 * 256, device=dev, dtype=e16))
         K.gemm(patches, self._w("patch.w", pe.weight, lambda t: t.reshape(D, -1)), M=M, N=D, K=3 * 256, out=x,
                bias=self._wf("patch.b", pe.bias), residual=self._wf("pos", self.pos_embed,
                                                                                    lambda t: t.reshape(L, D)),
                r_remap=(L, B))
-        xn = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
-        mlp_h = torch.empty(M, cfg.mlp_dim, device=dev, dtype=torch.bfloat16)
+        xn = torch.empty(M, D, device=dev, dtype=e16)
+        mlp_h = torch.empty(M, cfg.mlp_dim, device=dev, dtype=e16)
         wmap = None
         for li, layer in enumerate(self.layers):
             at = layer.attn
@@ -170,12 +174,12 @@ class VisionEncoder(nn.Module):
                 if wmap is None:
                     wmap = self._window_map(B, dev)
                 Mw = wmap.numel()
-                xw = torch.empty(Mw, D, device=dev, dtype=torch.bfloat16)
+                xw = torch.empty(Mw, D, device=dev, dtype=e16)
                 K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xw, src_rows=wmap)
-                qkv = torch.empty(Mw, 3 * D, device=dev, dtype=torch.bfloat16)
+                qkv = torch.empty(Mw, 3 * D, device=dev, dtype=e16)
                 K.gemm(xw, self._w(pre + "qkv", at.qkv.weight), M=Mw, N=3 * D, K=D, out=qkv,
                        bias=self._wf(pre + "qkvb", at.qkv.bias))
-                ao = torch.empty(Mw, D, device=dev, dtype=torch.bfloat16)
+                ao = torch.empty(Mw, D, device=dev, dtype=e16)
                 K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
                                 nseq=Mw // (ws * ws), side=ws, heads=heads)
                 K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=Mw, N=D, K=D, out=x,
@@ -183,10 +187,10 @@ class VisionEncoder(nn.Module):
                 del xw, qkv, ao
             else:
                 K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xn)
-                qkv = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+                qkv = torch.empty(M, 3 * D, device=dev, dtype=e16)
                 K.gemm(xn, self._w(pre + "qkv", at.qkv.weight), M=M, N=3 * D, K=D, out=qkv,
                        bias=self._wf(pre + "qkvb", at.qkv.bias))
-                ao = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+                ao = torch.empty(M, D, device=dev, dtype=e16)
                 K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
                                 nseq=B, side=g, heads=heads)
                 K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=M, N=D, K=D, out=x,
@@ -205,7 +209,7 @@ class VisionEncoder(nn.Module):
         nk = self.neck
         y = torch.empty(M, C, device=dev, dtype=torch.float32)
         K.gemm(xn, self._w("neck.c1", nk.conv1.weight, lambda t: t.reshape(C, D)), M=M, N=C, K=D, out=y)
-        yb = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+        yb = torch.empty(M, C, device=dev, dtype=e16)
         K.layernorm_fwd(y, self._wf("neck.ln1w", nk.layer_norm1.weight), self._wf("neck.ln1b", nk.layer_norm1.bias),
                         1e-6, yb)
         K.gemm(yb, self._w("neck.c2", nk.conv2.weight, lambda t: t.permute(0, 2, 3, 1).reshape(C, 9 * C)), M=M,
@@ -343,6 +347,15 @@ class SamModel(nn.Module):
                 val = torch.randn(p.shape, generator=gen) * std
             p.copy_(val.to(p.dtype))
         self.mask_decoder.sync_bf16()
+
+    def set_encoder_dtype(self, dtype) -> "SamModel":
+        """Operand type of the frozen image encoder's GEMMs and attention: torch.bfloat16 (default) or
+        torch.float16 (BASELINE configs[4]). The trainable mask decoder keeps fp32 master weights and bf16
+        operands (bf16's fp32 exponent range needs no loss scaling for its gradients)."""
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError("encoder dtype must be torch.bfloat16 or torch.float16")
+        self.vision_encoder.compute_dtype = dtype
+        return self
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         res = super().load_state_dict(state_dict, strict=strict, assign=False)

@@ -508,6 +508,8 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     rank = dist.get_rank(pg) if pg is not None else 0
     device = device or torch.device("cuda", torch.cuda.current_device())
     model = SamModel.from_pretrained(base_model, **({"seed": config["seed"]} if "seed" in config else {})).to(device)
+    if config.get("encoder_dtype", "bf16") == "fp16":  # BASELINE configs[4]
+        model.set_encoder_dtype(torch.float16)
     if device.type == "cuda" and config.get("gpu_processor", True):  # image path as a HIP kernel (§8(f)1)
         from .preprocess import DeviceProcessor
         processor = DeviceProcessor(device)
@@ -684,6 +686,8 @@ def build_parser():
                    help="topological loss: --top, --top=True or --top=False (README usage; the reference's "
                         "store_true flag rejects --top=True)")
     p.add_argument("--synthetic", type=int, default=0, help="train on K synthetic images (no dataset on disk)")
+    p.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp16"],
+                   help="16-bit operand type of the frozen image encoder (build extension; fp16 = configs[4])")
     return p
 
 
@@ -706,7 +710,7 @@ def main(argv=None):
               "learning_rate": args.lr, "weight_decay": args.weight_decay, "epochs": args.epochs,
               "batch_size": args.bs, "shuffle": args.shuffle, "optimizer": args.optimizer, "loss": args.loss,
               "time": now, "evaluate": args.evaluate, "topological": args.top, "prompt_type": args.prompt,
-              "pseudocolor": None}
+              "pseudocolor": None, "encoder_dtype": args.precision}
     pg = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:

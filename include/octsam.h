@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 8
+#define OCTSAM_ABI_VERSION 9
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -78,6 +78,9 @@ typedef struct octsam_gemm_args {
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);
+/* the same GEMM with IEEE-half 16-bit operands (A, B, and C / C_pre / R when not fp32): the fp16 encoder of
+ * BASELINE configs[4] (sam-vit-huge, fp16) */
+int octsam_gemm_f16(const octsam_gemm_args* args, void* stream);
 /* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing) */
 void octsam_gemm_set_fast_path(int32_t enable);
 /* 1 if the calling thread's last octsam_gemm launched the persistent global_load_lds kernel
@@ -111,8 +114,9 @@ int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, int32_t W, in
  * SamVisionLayer (hf:modeling_sam.py:954-972), SamVisionNeck (:975-992), SamTwoWayAttentionBlock
  * (:306-348), SamTwoWayTransformer (:363, eps 1e-5) and the mask-decoder upscaling (:519-521).
  * Forward: y[r] = act(LN(x[src_rows ? src_rows[r] : r])) over the last dim D in {64,256,768,1024,1280};
- * a negative src_rows[r] writes a zero row (window_partition padding, :900-922). y is bf16 or fp32
- * (y_f32); y2_f32 (optional) receives an fp32 copy; mean/rstd (optional, fp32 [rows]) are saved.
+ * a negative src_rows[r] writes a zero row (window_partition padding, :900-922). y is bf16 (y_f32 = 0), fp32
+ * (y_f32 = 1) or fp16 (y_f32 = 2, the fp16 encoder); y2_f32 (optional) receives an fp32 copy; mean/rstd
+ * (optional, fp32 [rows]) are saved.
  * Backward (D in {64,256,768}): dx = beta*dx + dLN (dx2_bf16 optional bf16 copy); per-block dw/db partials [nblocks, D] are written
  * to dw_part/db_part (combine with octsam_splitk_reduce). act must match the forward. */
 int octsam_layernorm_fwd(const void* x, int32_t x_f32, const int32_t* src_rows, int64_t rows, int32_t D,
@@ -159,11 +163,13 @@ int octsam_relu_bwd(const float* dy, const void* y, int64_t ldy, int32_t cols, v
  * (the backward of repeat_interleave, hf:modeling_sam.py:499-501). */
 int octsam_group_sum(const void* in, int64_t ld_in, int32_t cols, int32_t groups, int32_t nper, int64_t rows_per,
                      void* out, void* stream);
-/* bf16 copy of an fp32 buffer */
+/* bf16 / fp16 copy of an fp32 buffer */
 int octsam_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+int octsam_cast_f16(const float* x, void* y, int64_t n, void* stream);
 /* Patch-embedding operand: pixel_values fp32 [B, 3, 1024, 1024] -> bf16 [B*4096, 768], row = (b, py, px),
  * k = (c, ky, kx) (= Conv2d(3, D, 16, 16) weight.reshape(D, 768) order); replaces the gathered a_mode 2. */
 int octsam_patchify_bf16(const float* px, int32_t B, void* out, void* stream);
+int octsam_patchify_f16(const float* px, int32_t B, void* out, void* stream);  /* IEEE half rows */
 
 /* ---------------------------------------------------------------- label components (A2)
  * SAMDataset._components (ref:octsam/models/training_utils.py:389-434: np.unique values, scipy.ndimage.label

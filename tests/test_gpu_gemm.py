@@ -278,3 +278,59 @@ def test_gemm_small_path_ktotal(cuda):
     assert lib.octsam_gemm_last_path() == 3
     ref = dyb[:rows].float().t() @ xb[:rows].float()
     assert _rel(part.sum(0), ref) < 1e-5
+
+
+# ------------------------------------------------------------------ fp16 operands (octsam_gemm_f16)
+@pytest.mark.parametrize("M,N,K,res16", [(300, 200, 136, False), (4096, 768, 768, False), (8192, 3840, 1280, True),
+                                          (32768, 1280, 5120, False), (7, 40, 256, True)])
+def test_gemm_f16_encoder_paths(cuda, M, N, K, res16):
+    """The fp16 encoder's NT GEMMs (small 64-tile path, persistent LDS-DMA kernel, 8-phase kernel with the
+    register epilogue; fp32 or fp16 residual, GELU, fp16 / fp32 outputs) vs fp32 on the same fp16 operands.
+    fp16 keeps 11 significant bits: fp16 outputs are checked at 2e-3, fp32 outputs at 1e-5."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = (0.5 * torch.randn(M, K, generator=g)).to(cuda, torch.float16)
+    W = (0.5 * torch.randn(N, K, generator=g)).to(cuda, torch.float16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda, torch.float16 if res16 else torch.float32)
+    ref_pre = A.float() @ W.float().t() + bias
+    out32 = torch.empty(M, N, device=cuda)
+    kernels.gemm(A, W, M=M, N=N, K=K, out=out32, bias=bias, residual=R)
+    assert _rel(out32, ref_pre + R.float()) < (2e-3 if res16 else 1e-5)
+    out16 = torch.empty(M, N, device=cuda, dtype=torch.float16)
+    kernels.gemm(A, W, M=M, N=N, K=K, out=out16, bias=bias, act=2)
+    assert _rel(out16, F.gelu(ref_pre)) < 2e-3
+
+
+def test_gemm_f16_conv3x3_and_mixed_types_rejected(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(8)
+    C = 256
+    x = (0.5 * torch.randn(1, 64, 64, C, generator=g)).to(cuda, torch.float16)
+    w = (0.05 * torch.randn(C, C, 3, 3, generator=g)).to(cuda)
+    wk = w.permute(0, 2, 3, 1).reshape(C, 9 * C).to(torch.float16)
+    out = torch.empty(4096, C, device=cuda)
+    kernels.gemm(x.reshape(4096, C), wk, M=4096, N=C, K=9 * C, out=out, a_mode=3, conv_c=C)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wk.float().reshape(C, 3, 3, C).permute(0, 3, 1, 2), padding=1)
+    assert _rel(out, ref.permute(0, 2, 3, 1).reshape(4096, C)) < 1e-5
+    with pytest.raises(ValueError):
+        kernels.gemm(x.reshape(4096, C).to(torch.bfloat16), wk, M=4096, N=C, K=9 * C, out=out, a_mode=3, conv_c=C)
+
+
+def test_fp16_encoder_pieces(cuda):
+    """patchify, LayerNorm and the fp32 -> 16-bit cast with fp16 outputs."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(9)
+    px = torch.randn(1, 3, 1024, 1024, generator=g).to(cuda)
+    out = torch.empty(4096, 768, device=cuda, dtype=torch.float16)
+    kernels.patchify_bf16(px, out)
+    ref = px.view(1, 3, 64, 16, 64, 16).permute(0, 2, 4, 1, 3, 5).reshape(4096, 768).to(torch.float16)
+    assert torch.equal(out, ref)
+    x = torch.randn(1000, 1280, generator=g).to(cuda)
+    w, b = torch.randn(1280, generator=g).to(cuda), torch.randn(1280, generator=g).to(cuda)
+    y = torch.empty(1000, 1280, device=cuda, dtype=torch.float16)
+    kernels.layernorm_fwd(x, w, b, 1e-6, y)
+    assert _rel(y, F.layer_norm(x, (1280,), w, b, 1e-6)) < 1e-3
+    c = torch.empty(1000, 1280, device=cuda, dtype=torch.float16)
+    kernels.cast_bf16(x, c)
+    assert torch.equal(c, x.to(torch.float16))

@@ -57,3 +57,42 @@ def test_vit_huge_parity_and_step(cuda):
     print("vit-h step loss (dice, ce, topo, total):", lh.tolist())
     assert torch.isfinite(lh).all()
     assert not torch.equal(before, ours.mask_decoder.flat)
+
+
+def test_vit_huge_fp16_encoder(cuda):
+    """BASELINE configs[4] precision: the frozen encoder's GEMMs and attention on fp16 operands (octsam_gemm_f16,
+    fp16 attention), fp32 accumulation and residual stream; vs transformers fp32 (fp16's 11-bit significand:
+    tighter than the bf16 bound) and one fused training step."""
+    from transformers import SamModel as HFSam
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    from oracle.step_ref import hf_config
+    ours = SamModel(NAME)
+    ours.init_weights(seed=6)
+    hf = HFSam(hf_config(NAME))
+    hf.load_state_dict(ours.state_dict())
+    ours = ours.to(cuda).set_encoder_dtype(torch.float16)
+    hf = hf.to(cuda).float().eval()
+    px = torch.randn(2, 3, 1024, 1024, generator=torch.Generator().manual_seed(2)).to(cuda)
+    with torch.no_grad():
+        ref = hf.vision_encoder(px).last_hidden_state
+        got = ours.vision_encoder(px)
+    err16 = _rel(got, ref)
+    ours.set_encoder_dtype(torch.bfloat16)
+    with torch.no_grad():
+        err_b = _rel(ours.vision_encoder(px), ref)
+    ours.set_encoder_dtype(torch.float16)
+    print(f"vit-h encoder rel err fp16 {err16:.5f} (bf16 {err_b:.5f})")
+    assert err16 < 5e-3 and err16 < err_b
+    del hf
+    torch.cuda.empty_cache()
+    ds = data.synthetic_oct(seed=7, n=2)
+    sd = data.SAMDataset(ds, {"prompt_type": "both"}, epoch_seed=0)
+    b = data.to_device_batch(data.process_batch(data.make_processor(),
+                                                data.custom_collate([sd[i] for i in range(2)]), "both"), cuda)
+    step = FusedTrainStep(ours, lr=1e-3, topological=True, graphs=True)
+    for _ in range(2):
+        loss = step.step(b)
+    step.flush()
+    assert torch.isfinite(loss.cpu()).all()
