@@ -164,3 +164,11 @@ def call(name: str, *args) -> None:
 
 def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
+
+
+def resolve_device(device) -> torch.device:
+    """torch.device with an explicit index ("cuda" -> "cuda:<current>"), so device checks compare equal."""
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d

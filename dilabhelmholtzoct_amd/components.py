@@ -35,7 +35,7 @@ class DeviceComponents:
     """Connected components + component statistics of uint8 label maps on one device."""
 
     def __init__(self, device, max_components: int = MAX_COMPONENTS):
-        self.device = torch.device(device)
+        self.device = _lib.resolve_device(device)
         self.maxc = int(max_components)
         if not 1 <= self.maxc <= MAX_COMPONENTS:
             raise ValueError(f"max_components must be in [1, {MAX_COMPONENTS}]")
@@ -142,7 +142,7 @@ def _kth_pixels(cc: dict, ks: list, W: int) -> list:
 
 def collate_device_begin(images, labels, prompt_type: str, device, seed_hooks=None) -> dict:
     """Phase 1 of collate_device: upload, components; the state's ``ncomp`` sizes the (global) batch N."""
-    dev = torch.device(device)
+    dev = _lib.resolve_device(device)
     labels = torch.as_tensor(labels).to(dev)
     dc = DeviceComponents(dev)
     return {"dc": dc, "cc": dc.label(labels), "images": torch.as_tensor(images), "prompt_type": prompt_type,

@@ -7,10 +7,13 @@
 // scipy numbers the components of one value in raster order of their first pixel, and np.unique visits
 // values in increasing order, so the reference's component order is the order of the key
 // (value << 24 | first pixel index). Here:
-//   1. octsam_cc_label: lock-free union-find over the 8-neighbourhood (each pixel unites with its W, NW,
-//      N, NE neighbours of equal value; roots are hooked onto the smaller root with atomicMin, so every
-//      component ends rooted at its first raster pixel), then one flatten pass that also emits the key of
-//      every root into a per-image list (unordered, counted).
+//   1. octsam_cc_label: block union-find over the 8-neighbourhood (each pixel unites with its W, NW, N, NE
+//      neighbours of equal value; roots are hooked onto the smaller root with atomicMin, so every component
+//      ends rooted at its first raster pixel): each workgroup labels a 32 x 64 tile in LDS (LDS atomics,
+//      local indices are raster-monotone, so the local root is the tile's first pixel of the component) and
+//      writes global parents; a second pass unites only the pixels whose neighbours lie in another tile
+//      (lock-free, global atomicMin); one flatten pass then also emits the key of every root into a per-image
+//      list (unordered, counted).
 //   2. the host sorts each image's keys (a few dozen) -> component order;
 //   3. octsam_cc_assign: scatter the rank to the root pixels, give every pixel its root's rank, and reduce
 //      (xmin, xmax, ymin, ymax, pixel count) per component through LDS atomics into global atomics;
@@ -53,26 +56,91 @@ __device__ __forceinline__ void unite(int* P, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void cc_init_kernel(int* __restrict__ parent, int hw, int* __restrict__ nroots) {
-  const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
-  if (i < hw) parent[(long long)b * hw + i] = i;
-  if (i == 0) nroots[b] = 0;
+constexpr int TH = 32, TW = 64, TPIX = TH * TW;  // label tile (2048 pixels, 8 per thread)
+
+__device__ __forceinline__ int lds_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+__device__ __forceinline__ int lfind(const int* lp, int x) {
+  int p = lds_ld(lp + x);
+  while (p != x) {
+    x = p;
+    p = lds_ld(lp + x);
+  }
+  return x;
 }
 
-__global__ __launch_bounds__(256) void cc_merge_kernel(const uint8_t* __restrict__ lab, int H, int W,
-                                                       int* __restrict__ parent) {
+__device__ __forceinline__ void lunite(int* lp, int a, int b) {
+  while (true) {
+    a = lfind(lp, a);
+    b = lfind(lp, b);
+    if (a == b) return;
+    if (a > b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicMin(lp + b, a);
+    if (old == b) return;
+    b = old;
+  }
+}
+
+// one workgroup per (32 x 64 tile, image): union-find of the tile in LDS, then parent[p] = global index of the
+// pixel's tile-local root (roots point to themselves)
+__global__ __launch_bounds__(256) void cc_tile_kernel(const uint8_t* __restrict__ lab, int H, int W,
+                                                      int* __restrict__ parent, int* __restrict__ nroots) {
+  __shared__ int lp[TPIX];
+  __shared__ uint8_t lv[TPIX];
+  const int b = blockIdx.y, tiles_x = (W + TW - 1) / TW;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int x0 = tx * TW, y0 = ty * TH;
+  const long long hw = (long long)H * W;
+  const uint8_t* L = lab + b * hw;
+  if (blockIdx.x == 0 && threadIdx.x == 0) nroots[b] = 0;
+  for (int l = threadIdx.x; l < TPIX; l += 256) {
+    const int y = y0 + l / TW, x = x0 + l % TW;
+    lp[l] = l;
+    lv[l] = (y < H && x < W) ? L[(long long)y * W + x] : 0;
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < TPIX; l += 256) {
+    const int ly = l / TW, lx = l % TW, y = y0 + ly, x = x0 + lx;
+    if (y >= H || x >= W) continue;
+    const uint8_t v = lv[l];
+    if (lx > 0 && lv[l - 1] == v) lunite(lp, l, l - 1);
+    if (ly > 0) {
+      if (lx > 0 && lv[l - TW - 1] == v) lunite(lp, l, l - TW - 1);
+      if (lv[l - TW] == v) lunite(lp, l, l - TW);
+      if (lx + 1 < TW && x + 1 < W && lv[l - TW + 1] == v) lunite(lp, l, l - TW + 1);
+    }
+  }
+  __syncthreads();
+  int* P = parent + b * hw;
+  for (int l = threadIdx.x; l < TPIX; l += 256) {
+    const int y = y0 + l / TW, x = x0 + l % TW;
+    if (y >= H || x >= W) continue;
+    const int r = lfind(lp, l);
+    P[(long long)y * W + x] = (y0 + r / TW) * W + x0 + r % TW;
+  }
+}
+
+// the neighbour pairs that cross a tile boundary, united in the global forest
+__global__ __launch_bounds__(256) void cc_border_kernel(const uint8_t* __restrict__ lab, int H, int W,
+                                                        int* __restrict__ parent) {
   const int hw = H * W;
   const int i = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
   if (i >= hw) return;
+  const int y = i / W, x = i - y * W;
+  const bool left = x > 0 && x % TW == 0, top = y > 0 && y % TH == 0, right = x % TW == TW - 1 && x + 1 < W;
+  if (!left && !top && !(right && y > 0)) return;
   const uint8_t* L = lab + (long long)b * hw;
   int* P = parent + (long long)b * hw;
-  const int y = i / W, x = i - y * W;
   const uint8_t v = L[i];
-  if (x > 0 && L[i - 1] == v) unite(P, i, i - 1);
+  if (left && L[i - 1] == v) unite(P, i, i - 1);
   if (y > 0) {
-    if (x > 0 && L[i - W - 1] == v) unite(P, i, i - W - 1);
-    if (L[i - W] == v) unite(P, i, i - W);
-    if (x + 1 < W && L[i - W + 1] == v) unite(P, i, i - W + 1);
+    if (x > 0 && (left || top) && L[i - W - 1] == v) unite(P, i, i - W - 1);
+    if (top && L[i - W] == v) unite(P, i, i - W);
+    if (x + 1 < W && (right || top) && L[i - W + 1] == v) unite(P, i, i - W + 1);
   }
 }
 
@@ -178,8 +246,9 @@ extern "C" int octsam_cc_label(const uint8_t* labels, int32_t B, int32_t H, int3
   hipStream_t s = (hipStream_t)stream;
   const int hw = H * W;
   const dim3 grid((hw + 255) / 256, B);
-  hipLaunchKernelGGL(cc_init_kernel, grid, dim3(256), 0, s, parent, hw, nroots);
-  hipLaunchKernelGGL(cc_merge_kernel, grid, dim3(256), 0, s, labels, H, W, parent);
+  const int ntiles = ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
+  hipLaunchKernelGGL(cc_tile_kernel, dim3(ntiles, B), dim3(256), 0, s, labels, H, W, parent, nroots);
+  hipLaunchKernelGGL(cc_border_kernel, grid, dim3(256), 0, s, labels, H, W, parent);
   hipLaunchKernelGGL(cc_flatten_kernel, grid, dim3(256), 0, s, labels, hw, parent, roots, max_roots, nroots);
   OCTSAM_LAUNCH_CHECK("octsam_cc_label");
   return 0;

@@ -101,7 +101,7 @@ class DeviceProcessor:
 
     def __init__(self, device, mean=IMAGENET_MEAN, std=IMAGENET_STD, rescale: float = 1 / 255,
                  longest_edge: int = LONGEST_EDGE):
-        self.device = torch.device(device)
+        self.device = _lib.resolve_device(device)
         self.longest_edge = longest_edge
         self.lut = torch.from_numpy(normalize_lut(mean, std, rescale)).to(self.device)
         self._tables = {}
