@@ -39,6 +39,15 @@ DEC_BWD_BYTES_PER_PROMPT = 24 * _E
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_gemm8.json")
 
 
+def traffic_json(args) -> str:
+    """PMC traffic file of the dominant GEMM for this workload (collected on the same bench flags by
+    scripts/gpu_round.sh): vit-base bf16 -> traffic_gemm8.json, otherwise traffic_gemm8_<model>_<dtype>.json."""
+    short = args.model.rsplit("/", 1)[-1]
+    if short == "sam-vit-base" and args.dtype == "bf16":
+        return TRAFFIC_JSON
+    return os.path.join(ROOT, "profiles", f"traffic_gemm8_{short}_{args.dtype}.json")
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -68,7 +77,10 @@ def parse():
     return p.parse_args()
 
 
-DOMINANT = "gemm8_kernel<0, EPI> (8-phase 256x256 bf16 NT GEMM: encoder QKV/proj/MLP, neck, decoder projections)"
+def dominant_name(args) -> str:
+    e = "bf16" if args.dtype == "bf16" else "fp16 (encoder) / bf16 (decoder)"
+    return (f"gemm8_kernel<0, EPI> (8-phase 256x256 {e} NT GEMM: encoder QKV/proj/MLP, neck, decoder "
+            "projections)")
 
 
 class GemmEventTimer:
@@ -508,12 +520,13 @@ def main():
         if n:
             achieved = flops / (ms * 1e-3) / 1e12
             traffic = None
-            if os.path.exists(TRAFFIC_JSON):
-                traffic = round(json.load(open(TRAFFIC_JSON))["hbm_bytes_per_launch"])
-            roof = {"bound": "mfma", "kernel": DOMINANT,
+            tj = traffic_json(args)
+            if os.path.exists(tj):
+                traffic = round(json.load(open(tj))["hbm_bytes_per_launch"])
+            roof = {"bound": "mfma", "kernel": dominant_name(args),
                     "achieved": round(achieved, 2), "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / MI355X_BF16_DENSE_TFLOPS, 4), "traffic": traffic,
-                    "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic is not None else None,
+                    "traffic_source": os.path.relpath(tj, ROOT) if traffic is not None else None,
                     "compulsory_bytes_per_launch": round(timer.bytes / n),
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}

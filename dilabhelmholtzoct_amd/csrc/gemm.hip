@@ -1455,9 +1455,22 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 
 }  // namespace
 
-static int g_use_glds = 1;
-static int g_small = 1;
-static thread_local int t_last_path = 0;
+// launch options and the last path taken are shared by the bf16 and fp16 builds of this file (the bf16
+// build owns them; the fp16 build reaches them through these hidden accessors), so
+// octsam_gemm_set_fast_path / octsam_gemm_last_path cover both entry points
+namespace __attribute__((visibility("hidden"))) octsam_gemm_state {
+int& use_glds();
+int& small_path();
+int& last_path();
+#ifndef OCTSAM_GEMM_F16
+int& use_glds() { static int v = 1; return v; }
+int& small_path() { static int v = 1; return v; }
+int& last_path() { static thread_local int v = 0; return v; }
+#endif
+}  // namespace octsam_gemm_state
+#define g_use_glds (octsam_gemm_state::use_glds())
+#define g_small (octsam_gemm_state::small_path())
+#define t_last_path (octsam_gemm_state::last_path())
 #ifndef OCTSAM_GEMM_F16
 // enable: 0 = generic kernels only; 1 = default; 2..10 = fast-path variants (diagnostics); bit 8 (256)
 // disables the small-problem 64x64 path
