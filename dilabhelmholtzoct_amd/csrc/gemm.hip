@@ -101,6 +101,7 @@ struct GemmK {
   int conv_c;  // channels for conv3x3 mode
   int tiles_m, tiles_n;
   int k_total;  // split-K over k-major operands: rows >= k_total (counted from batch 0) read as zero
+  int fast_epi;  // 8-phase kernels: e16 C (+ optional e16 residual) without row map / C_pre, 32-bit offsets
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -724,6 +725,7 @@ int launch_glds(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 // run one barrier apart so one row's MFMAs overlap the other's LDS reads.
 namespace ph8 {
 constexpr int BUF = 65536;  // A [256][64] + B [256][64] e16
+constexpr int BIAS_MAX_LDS = 8192;  // fp32 bias entries the persistent kernel keeps in LDS (32 KiB)
 
 // region 0 A-lo, 1 A-hi, 2 B-n0, 3 B-n1: 128 rows x 128 B = 16 instructions of 8 rows, 2 per wave
 __device__ __forceinline__ void load_region(const GemmK& p, const e16* A, const e16* B, int region, int row0,
@@ -743,6 +745,49 @@ __device__ __forceinline__ void load_region(const GemmK& p, const e16* A, const 
     gr = gr < lim ? gr : lim - 1;
     const e16* g = src + (long long)gr * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(buf + (isA ? 0 : 32768) + rbase * 128), 16, 0, 0);
+  }
+}
+
+// Tile-invariant part of load_region's addresses: byte offset (r * ld + c * 8) * 2 of each lane's 16-B
+// chunk for region / issue u. A full tile (no clamped rows) then needs one uniform base per operand and
+// K-step (SGPRs) and one add per issue, instead of a 64-bit multiply-add per lane and issue.
+struct LdPlan {
+  uint32_t off[4][2];
+};
+__device__ __forceinline__ LdPlan make_plan(const GemmK& p, int wave, int lane) {
+  LdPlan pl;
+#pragma unroll
+  for (int region = 0; region < 4; ++region)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool isA = region < 2;
+      const int j = wave * 2 + u;
+      const int rbase = isA ? (j >> 3) * 128 + (region & 1) * 64 + (j & 7) * 8
+                            : (j >> 2) * 64 + (region & 1) * 32 + (j & 3) * 8;
+      const int r = rbase + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ ((r >> 1) & 7);
+      pl.off[region][u] = (uint32_t)((r * (isA ? p.lda : p.ldb) + c * 8) * 2);
+    }
+  return pl;
+}
+// Buffer-descriptor form (persistent kernel): the descriptor starts at the tile's first row and ends at the
+// operand's last row, so rows past M (N) read as zero through the hardware range check (no clamp, no
+// per-lane 64-bit address); voffset = the tile-invariant plan offset, soffset = the K-step's byte offset.
+// Requires rows_left * ld * 2 < 2^31 (host-checked).
+__device__ __forceinline__ void load_region_buf(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int kt,
+                                                int region, const LdPlan& pl, char* buf, int wave) {
+  const bool isA = region < 2;
+  const e16* base = isA ? A + (long long)row0 * p.lda : B + (long long)col0 * p.ldb;
+  const long long ld = isA ? p.lda : p.ldb;
+  const int bytes = (int)((long long)((isA ? p.M - row0 : p.N - col0)) * ld * 2);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = wave * 2 + u;
+    const int rbase = isA ? (j >> 3) * 128 + (region & 1) * 64 + (j & 7) * 8
+                          : (j >> 2) * 64 + (region & 1) * 32 + (j & 3) * 8;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(buf + (isA ? 0 : 32768) + rbase * 128), 16,
+                                             pl.off[region][u], (uint32_t)(kt * 128), 0, 0);
   }
 }
 
@@ -948,43 +993,77 @@ __device__ __forceinline__ float act_apply(float v) {
   else return v;
 }
 
-template <int ACT>
+// MI0 / NMI: the row blocks mi in [MI0, MI0 + NMI) this call finishes (the persistent kernel runs two
+// halves of 4 so the epilogue's temporaries fit beside the live prefetch state)
+// BIAS_LDS: the bias comes from lds_bias (indexed by output column) and the epilogue issues no global
+// loads at all: no residual, no row map (the host routes those elsewhere)
+template <int ACT, int MI0 = 0, int NMI = 8, bool BIAS_LDS = false>
 __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0,
-                                             int lane) {
+                                             int lane, const float* lds_bias = nullptr) {
   char* Cb = (char*)p.C + bz * p.sC * (p.c_f32 ? 4 : 2);
-  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  const char* Rb = (!BIAS_LDS && p.R) ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
   char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
   const int q = lane >> 4;
   const int cofs = 16 * (q & 1) + 8 * (q >> 1);
   // permute first (all lanes active), then everything is per-lane elementwise on 8 consecutive columns
-  float v[8][2][8];
+  float v[NMI][2][8];
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
+  for (int j = 0; j < NMI; ++j)
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       // (bit-cast the whole vector first: hipcc 7.2 drops all but element 0 of a per-element
       // __builtin_bit_cast(uint32_t, f32x4[i]) feeding this builtin)
-      const u32x4 x = __builtin_bit_cast(u32x4, acc[mi][2 * pr]), y = __builtin_bit_cast(u32x4, acc[mi][2 * pr + 1]);
+      const u32x4 x = __builtin_bit_cast(u32x4, acc[MI0 + j][2 * pr]);
+      const u32x4 y = __builtin_bit_cast(u32x4, acc[MI0 + j][2 * pr + 1]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t xi = x[i], yi = y[i];
         const auto r = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
-        v[mi][pr][i] = __builtin_bit_cast(float, (uint32_t)r[0]);
-        v[mi][pr][4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
+        v[j][pr][i] = __builtin_bit_cast(float, (uint32_t)r[0]);
+        v[j][pr][4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
       }
     }
-  int om[8];
+  int om[NMI];
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = row0 + 16 * mi + (lane & 15);
-    om[mi] = m < p.M ? (p.row_map ? p.row_map[m] : m) : -1;
+  for (int j = 0; j < NMI; ++j) {
+    const int m = row0 + 16 * (MI0 + j) + (lane & 15);
+    om[j] = m < p.M ? ((!BIAS_LDS && p.row_map) ? p.row_map[m] : m) : -1;
   }
   float bv[2][8];
+  if constexpr (BIAS_LDS) {
+    // read through inline asm: hipcc would put a vmcnt(0) (the in-flight LDS-DMA prefetch) in front of an
+    // ordinary LDS load here; the bias region is never a DMA target, so only lgkmcnt matters
+    if (p.bias) {
+      f32x4 t[2][2];
 #pragma unroll
-  for (int pr = 0; pr < 2; ++pr) {
+      for (int pr = 0; pr < 2; ++pr) {
+        const int n = min(col0 + 32 * pr + cofs, BIAS_MAX_LDS - 8);  // columns >= N are never stored
+        const uint32_t ad = (uint32_t)(uintptr_t)(lds_ptr_t)(lds_bias + n);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(t[pr][0]) : "v"(ad));
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(t[pr][1]) : "v"(ad));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bv[pr][e] = t[pr][0][e];
+          bv[pr][4 + e] = t[pr][1][e];
+        }
+    } else {
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[pr][e] = 0.0f;
+    }
+  }
+#pragma unroll
+  for (int pr = 0; pr < 2 && !BIAS_LDS; ++pr) {
     const int n = col0 + 32 * pr + cofs;
     if (p.bias && n < p.N) {
-      const float4 a = *(const float4*)(p.bias + n), b = *(const float4*)(p.bias + n + 4);
+      const float* bsrc = p.bias;
+      const float4 a = *(const float4*)(bsrc + n), b = *(const float4*)(bsrc + n + 4);
       bv[pr][0] = a.x; bv[pr][1] = a.y; bv[pr][2] = a.z; bv[pr][3] = a.w;
       bv[pr][4] = b.x; bv[pr][5] = b.y; bv[pr][6] = b.z; bv[pr][7] = b.w;
     } else {
@@ -993,77 +1072,170 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
     }
   }
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
+  for (int j = 0; j < NMI; ++j)
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[mi][pr][e] = v[mi][pr][e] * p.alpha + bv[pr][e];
+      for (int e = 0; e < 8; ++e) v[j][pr][e] = v[j][pr][e] * p.alpha + bv[pr][e];
   // (beta != 0 is routed to the other kernels by the host)
-  auto finish = [&](int mi, int pr, const float (&res)[8]) {
+  auto finish = [&](int j, int pr, const float (&res)[8]) {
     const int n = col0 + 32 * pr + cofs;
-    const bool ok = om[mi] >= 0 && n < p.N;
-    const long long ci = (long long)om[mi] * p.ldc + n;
-    if (Pb && ok) store8(Pb, ci, p.pre_f32, v[mi][pr]);
+    const bool ok = om[j] >= 0 && n < p.N;
+    const long long ci = (long long)om[j] * p.ldc + n;
+    if (Pb && ok) store8(Pb, ci, p.pre_f32, v[j][pr]);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[mi][pr][e] = act_apply<ACT>(v[mi][pr][e]) + res[e];
-    if (ok) store8(Cb, ci, p.c_f32, v[mi][pr]);
+    for (int e = 0; e < 8; ++e) v[j][pr][e] = act_apply<ACT>(v[j][pr][e]) + res[e];
+    if (ok) store8(Cb, ci, p.c_f32, v[j][pr]);
   };
   if (Rb && !p.r_f32) {
-    u32x4 raw[8][2];
+    u32x4 raw[NMI][2];
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int j = 0; j < NMI; ++j)
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int n = col0 + 32 * pr + cofs;
-        raw[mi][pr] = (om[mi] >= 0 && n < p.N)
-                          ? *(const u32x4*)((const e16*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n)
-                          : (u32x4)0u;
+        raw[j][pr] = (om[j] >= 0 && n < p.N)
+                         ? *(const u32x4*)((const e16*)Rb + remap(om[j], p.r_blk, p.r_rep) * p.ldr + n)
+                         : (u32x4)0u;
       }
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int j = 0; j < NMI; ++j)
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         float res[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          res[2 * e] = lo16f(raw[mi][pr][e]);
-          res[2 * e + 1] = hi16f(raw[mi][pr][e]);
+          res[2 * e] = lo16f(raw[j][pr][e]);
+          res[2 * e + 1] = hi16f(raw[j][pr][e]);
         }
-        finish(mi, pr, res);
+        finish(j, pr, res);
       }
-  } else if (Rb) {  // fp32 residual: two halves of 4 row blocks (register budget)
+  } else if (Rb) {  // fp32 residual: groups of 4 row blocks (register budget)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NMI / 4; ++h) {
       float4 raw[4][2][2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
-          const int mi = 4 * h + j, n = col0 + 32 * pr + cofs;
-          if (om[mi] >= 0 && n < p.N) {
-            const float* s = (const float*)Rb + remap(om[mi], p.r_blk, p.r_rep) * p.ldr + n;
-            raw[j][pr][0] = *(const float4*)s;
-            raw[j][pr][1] = *(const float4*)(s + 4);
+          const int j = 4 * h + jj, n = col0 + 32 * pr + cofs;
+          if (om[j] >= 0 && n < p.N) {
+            const float* s = (const float*)Rb + remap(om[j], p.r_blk, p.r_rep) * p.ldr + n;
+            raw[jj][pr][0] = *(const float4*)s;
+            raw[jj][pr][1] = *(const float4*)(s + 4);
           } else {
-            raw[j][pr][0] = raw[j][pr][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            raw[jj][pr][0] = raw[jj][pr][1] = make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
-          const float res[8] = {raw[j][pr][0].x, raw[j][pr][0].y, raw[j][pr][0].z, raw[j][pr][0].w,
-                                raw[j][pr][1].x, raw[j][pr][1].y, raw[j][pr][1].z, raw[j][pr][1].w};
-          finish(4 * h + j, pr, res);
+          const float res[8] = {raw[jj][pr][0].x, raw[jj][pr][0].y, raw[jj][pr][0].z, raw[jj][pr][0].w,
+                                raw[jj][pr][1].x, raw[jj][pr][1].y, raw[jj][pr][1].z, raw[jj][pr][1].w};
+          finish(4 * h + jj, pr, res);
         }
     }
   } else {
     const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int j = 0; j < NMI; ++j)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr) finish(mi, pr, zero);
+      for (int pr = 0; pr < 2; ++pr) finish(j, pr, zero);
   }
+}
+
+// Lean register epilogue for a tile whose 256 columns are all inside N, e16 C, no row map / C_pre: C (and an
+// e16 residual) go through buffer descriptors that start at the wave's first row and end at row M, so rows
+// past M are dropped (stores) or read as zero (residual) by the hardware range check, and every store is
+// one voffset add + buffer_store_dwordx4. RES: e16 residual; BIAS_LDS: bias read from LDS (persistent
+// kernel), else from global. Host guarantees M * ldc * 2 and M * ldr * 2 < 2^31 (fast_epi).
+template <int ACT, bool RES, bool BIAS_LDS, int MI0 = 0, int NMI = 8>
+__device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0,
+                                              int lane, const float* lds_bias = nullptr) {
+  const int q = lane >> 4;
+  const int cofs = 16 * (q & 1) + 8 * (q >> 1);
+  const int rows_left = max(0, p.M - row0);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((e16*)p.C + bz * p.sC + (long long)row0 * p.ldc + col0), (short)0, (int)(rows_left * p.ldc * 2),
+      0x00020000);
+  const uint32_t vb = (uint32_t)(((lane & 15) * p.ldc + cofs) * 2);
+  float v[NMI][2][8];
+#pragma unroll
+  for (int j = 0; j < NMI; ++j)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const u32x4 x = __builtin_bit_cast(u32x4, acc[MI0 + j][2 * pr]);
+      const u32x4 y = __builtin_bit_cast(u32x4, acc[MI0 + j][2 * pr + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t xi = x[i], yi = y[i];
+        const auto r = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
+        v[j][pr][i] = __builtin_bit_cast(float, (uint32_t)r[0]);
+        v[j][pr][4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
+      }
+    }
+  float bv[2][8];
+  if (p.bias) {
+    f32x4 t[2][2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int n = col0 + 32 * pr + cofs;
+      if constexpr (BIAS_LDS) {
+        // inline asm: hipcc would put a vmcnt(0) (the in-flight LDS-DMA prefetch) in front of an ordinary
+        // LDS load; the bias region is never a DMA target
+        const uint32_t ad = (uint32_t)(uintptr_t)(lds_ptr_t)(lds_bias + n);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(t[pr][0]) : "v"(ad));
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(t[pr][1]) : "v"(ad));
+      } else {
+        t[pr][0] = *(const f32x4*)(p.bias + n);
+        t[pr][1] = *(const f32x4*)(p.bias + n + 4);
+      }
+    }
+    if constexpr (BIAS_LDS) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[pr][e] = t[pr][0][e];
+        bv[pr][4 + e] = t[pr][1][e];
+      }
+  } else {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[pr][e] = 0.0f;
+  }
+  u32x4 raw[RES ? NMI : 1][2];
+  if constexpr (RES) {
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const e16*)p.R + bz * p.sR + (long long)row0 * p.ldr + col0), (short)0,
+        (int)(rows_left * p.ldr * 2), 0x00020000);
+    const uint32_t rb = (uint32_t)(((lane & 15) * p.ldr + cofs) * 2);
+#pragma unroll
+    for (int j = 0; j < NMI; ++j)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        raw[j][pr] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, rb + (uint32_t)((16 * (MI0 + j) * p.ldr + 32 * pr) * 2), 0, 0));
+  }
+#pragma unroll
+  for (int j = 0; j < NMI; ++j)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      e16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = act_apply<ACT>(v[j][pr][e] * p.alpha + bv[pr][e]);
+        if constexpr (RES) t += (e & 1) ? hi16f(raw[j][pr][e >> 1]) : lo16f(raw[j][pr][e >> 1]);
+        o[e] = (e16)t;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc,
+                                             vb + (uint32_t)((16 * (MI0 + j) * p.ldc + 32 * pr) * 2), 0, 0);
+    }
 }
 }  // namespace ph8
 
@@ -1078,8 +1250,10 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
            : mma16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
 
-// EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA)
-template <int DBG, int EPI>
+// EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA).
+// FE: 0 = general register epilogue, 1 = lean buffer-store epilogue, 2 = lean with an e16 residual (both need
+// N % 256 == 0 and fast_epi; one epilogue per instantiation keeps the register allocation spill-free)
+template <int DBG, int EPI, int FE = 0>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   constexpr bool TR = EPI >= 0;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
@@ -1186,25 +1360,43 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     if (x == 12345.f) ((float*)p.C)[0] = x;
     return;
   }
-  if constexpr (TR) ph8::epilogue_reg<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
-  else ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
+  if constexpr (TR) {
+    if constexpr (FE == 2) {
+      ph8::epilogue_fast<EPI, true, false, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+      ph8::epilogue_fast<EPI, true, false, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    } else if constexpr (FE == 1) {
+      ph8::epilogue_fast<EPI, false, false>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    } else {
+      ph8::epilogue_reg<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    }
+  } else {
+    ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
+  }
 }
 
-template <int DBG, int EPI>
-int launch_gemm8(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+template <int DBG, int EPI, int FE = 0>
+int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + 255) / 256;
   constexpr int LDS = EPI < 0 ? ph8::EPI_BYTES : 2 * ph8::BUF;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8_kernel<DBG, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    (void)hipFuncSetAttribute((const void*)gemm8_kernel<DBG, EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS);
     attr = true;
   }
   const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
-  hipLaunchKernelGGL((gemm8_kernel<DBG, EPI>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
+  hipLaunchKernelGGL((gemm8_kernel<DBG, EPI, FE>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
+}
+
+template <int DBG, int EPI>
+int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
+  if (EPI >= 0 && DBG == 0 && k.fast_epi && a->N % 256 == 0)
+    return a->R ? launch_gemm8_fe<DBG, EPI, 2>(k, a, s) : launch_gemm8_fe<DBG, EPI, 1>(k, a, s);
+  return launch_gemm8_fe<DBG, EPI, 0>(k, a, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1233,19 +1425,27 @@ __device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, 
   c.kt = 0;
   return c;
 }
+// counted vmcnt wait; relax: the ST_PER_EPI stores of the previous tile's epilogue were issued after the
+// operation this wait retires, so they are added to the count (they drain under the MFMAs instead)
+constexpr int ST_PER_EPI = 16;
 template <int BASE>
 __device__ __forceinline__ void vm_wait(bool relax) {
-  // relax: the 16 store instructions of a full e16 tile's epilogue sit above the loads this wait retires
-  (void)relax;
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE) : "memory");
+  if (relax) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE + ST_PER_EPI) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE) : "memory");
 }
+constexpr int BIAS_MAX = BIAS_MAX_LDS;
 }  // namespace ph8
 
-template <int EPI>
-__global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
+// Persistent variant for bias / activation epilogues (no residual, no row map): the bias vector lives in LDS
+// (copied once per workgroup before the first prefetch), so the epilogue issues no vector-memory loads and
+// the compiler never drains the in-flight prefetch of the next tile; only stores follow it, and for a full
+// e16 tile (exactly ST_PER_EPI store instructions per wave) the first waits of the next tile count them
+// (relaxed) rather than waiting for them.
+template <int EPI, int FE>
+__global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int dbg) {
   constexpr bool TR = true;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int per_batch = p.tiles_m * p.tiles_n;
   const int ntiles = per_batch * batch;
@@ -1258,9 +1458,17 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
   const int nk = p.K / 64;
   const int G = mycnt * nk;
   if (G == 0) return;
-  // only e16-output epilogues without a pre-activation copy have the exact 16-store count the relaxed
-  // waits assume; everything else waits for its stores (conservative)
-  const bool relax_ok = !p.c_f32 && p.Cpre == nullptr && p.row_map == nullptr;
+  float* lbias = (float*)(gsm + 2 * ph8::BUF);
+  if (p.bias) {  // whole bias vector -> LDS (N <= BIAS_MAX, N % 8 == 0: host-checked)
+    for (int i = tid * 4; i < p.N; i += 512 * 4) *(float4*)(lbias + i) = *(const float4*)(p.bias + i);
+  }
+  // only e16-output epilogues without a pre-activation copy have the exact store count the relaxed waits
+  // assume; everything else waits for its stores (conservative)
+  // relaxed waits are opt-in (fast path 13): measured slower on the encoder shapes — the next tile's loads
+  // then queue behind the stores instead of after them
+  const bool relax_ok = !p.c_f32 && p.Cpre == nullptr && (dbg & 1) && !(dbg & 4);
+  GemmK pe = p;          // the epilogue's view (diagnostics: 4 = no stores, 8 = every tile stores to tile 0)
+  if (dbg & 4) pe.M = 0;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1276,11 +1484,13 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
     if (++c.kt == nk) c = ph8::tile_cursor(p, c.i + 1, first, stride, per_batch);
     return c;
   };
+  const ph8::LdPlan plan = ph8::make_plan(p, wave, lane);
   auto issue = [&](const ph8::Cursor& c, int region, char* buf) {
-    ph8::load_region(p, c.A, c.B, region, c.row0, c.col0, c.kt * 64, buf, wave, lane);
+    ph8::load_region_buf(p, c.A, c.B, c.row0, c.col0, c.kt, region, plan, buf, wave);
   };
   ph8::Cursor c1 = advance(cc);
   ph8::Cursor c2 = advance(c1);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // bias copy done before the DMA count starts
   issue(cc, 0, gsm);
   issue(cc, 2, gsm);
   issue(cc, 3, gsm);
@@ -1296,13 +1506,17 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
   raw_barrier();
   if (wr == 1) raw_barrier();
 
-  bool relax = false;  // a full tile's epilogue stores sit above this step's first waits
+  // since: K-steps since the last epilogue (1: every wait of this step has the stores above the operation it
+  // retires; 2: only phase 0's does); relax: the last epilogue issued exactly ST_PER_EPI stores
+  int since = 3;
+  bool relax_epi = false;
   for (int g = 0; g < G; ++g) {
     char* cur = gsm + (g & 1) * ph8::BUF;
     char* nxt = gsm + ((g + 1) & 1) * ph8::BUF;
     const char* ca = cur;
     const char* cb = cur + 32768;
     const bool h1 = g + 1 < G, h2 = g + 2 < G;
+    const bool rx1 = relax_epi && since == 1, rx0 = relax_epi && since <= 2;
     // ---- phase 0: Q(0,0) — A-lo, B-n0
     if (h1) issue(c1, 1, nxt);
 #pragma unroll
@@ -1312,7 +1526,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) b0[ni][kb] = ph8::frag(cb, brow + ni * 16, kb * 4 + kq);
     }
-    if (h1) ph8::vm_wait<10>(relax);  // retire B-n1(g)
+    if (h1) ph8::vm_wait<10>(rx0);  // retire B-n1(g)
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1323,7 +1537,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) b1[ni][kb] = ph8::frag(cb, brow + 32 + ni * 16, kb * 4 + kq);
-    if (h1) ph8::vm_wait<8>(relax);  // retire A-hi(g)
+    if (h1) ph8::vm_wait<8>(rx1);  // retire A-hi(g)
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1344,20 +1558,28 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
     raw_barrier();
     // ---- phase 3: Q(1,1); restage B-n1 of step g+2; retire A-lo, B-n0 of step g+1
     if (h2) issue(c2, 3, cur);
-    if (h2) ph8::vm_wait<10>(relax);
-    else if (h1) ph8::vm_wait<4>(relax);
+    if (h2) ph8::vm_wait<10>(rx1);
+    else if (h1) ph8::vm_wait<4>(rx1);
     raw_barrier();
     PH8_MFMA_QUAD(1, 1, b1)
     raw_barrier();
-    relax = false;
+    ++since;
     if (++cc.kt == nk) {  // last K-step of tile cc.i: epilogue while steps g+1, g+2 load
-      ph8::epilogue_reg<EPI>(p, acc, (int)((first + cc.i * stride) / per_batch), cc.row0 + wr * 128,
-                             cc.col0 + wc * 64, lane);
+      const int ebz = (dbg & 8) ? 0 : (first + cc.i * stride) / per_batch;
+      const int er0 = ((dbg & 8) ? 0 : cc.row0) + wr * 128, ec0 = ((dbg & 8) ? 0 : cc.col0) + wc * 64;
+      if constexpr (FE == 1) {
+        ph8::epilogue_fast<EPI, false, true, 0, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
+        ph8::epilogue_fast<EPI, false, true, 4, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
+      } else {
+        ph8::epilogue_reg<EPI, 0, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
+        ph8::epilogue_reg<EPI, 4, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
+      }
 #pragma unroll
       for (int a = 0; a < 8; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4)0.0f;
-      relax = relax_ok && cc.row0 + 256 <= p.M && cc.col0 + 256 <= p.N;
+      relax_epi = relax_ok && cc.row0 + 256 <= p.M && cc.col0 + 256 <= p.N;
+      since = 1;
       cc = c1;  // (c1 is tile cc.i + 1 at K-tile 0 here)
     }
     c1 = c2;
@@ -1366,15 +1588,15 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch) {
   if (wr == 0) raw_barrier();  // balance the stagger
 }
 
-template <int EPI>
-int launch_gemm8p(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+template <int EPI, int FE>
+int launch_gemm8p_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, int dbg) {
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + 255) / 256;
-  constexpr int LDS = 2 * ph8::BUF;
+  constexpr int LDS = 2 * ph8::BUF + ph8::BIAS_MAX * 4;
   static int n_cu = 0;
   if (!n_cu) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     int dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1383,9 +1605,15 @@ int launch_gemm8p(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   const long long ntiles = (long long)g.tiles_m * g.tiles_n * a->batch;
   long long grid = ((n_cu + 7) / 8) * 8;
   while (grid > 8 && grid / 2 >= ntiles) grid /= 2;
-  hipLaunchKernelGGL((gemm8p_kernel<EPI>), dim3((unsigned)grid), dim3(512), LDS, s, g, a->batch);
+  if (dbg & 2) grid = (ntiles + 7) / 8 * 8;  // diagnostics: one tile per workgroup
+  hipLaunchKernelGGL((gemm8p_kernel<EPI, FE>), dim3((unsigned)grid), dim3(512), LDS, s, g, a->batch, dbg);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
+}
+template <int EPI>
+int launch_gemm8p(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, int dbg) {
+  if (k.fast_epi && a->N % 256 == 0) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
+  return launch_gemm8p_fe<EPI, 0>(k, a, s, dbg);
 }
 
 // Deterministic split reduction: out[i] = sum_s part[s*n + i] (+ beta*out[i]).
@@ -1514,6 +1742,10 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
   k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
   k.k_total = a->k_total;
+  k.fast_epi = !a->c_f32 && a->C_pre == nullptr && a->row_map == nullptr && (a->ldc & 7) == 0 &&
+               ((uintptr_t)a->C & 15) == 0 && (long long)a->M * a->ldc * 2 < (1LL << 31) &&
+               (a->R == nullptr || (!a->r_f32 && a->r_blk == 0 && (a->ldr & 7) == 0 && ((uintptr_t)a->R & 15) == 0 &&
+                                    (long long)a->M * a->ldr * 2 < (1LL << 31)));
   OCTSAM_CHECK_ARG(a->k_total == 0 || (a->a_mode == 1 && a->b_mode == 1 && a->k_total <= (long long)a->K * a->batch &&
                                        a->k_total > (long long)a->K * (a->batch - 1)),
                    "octsam_gemm: k_total needs a_mode = b_mode = 1 and (batch-1)*K < k_total <= batch*K");
@@ -1564,11 +1796,19 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       if (g_use_glds == 6) return launch_gemm8<1, 0>(k, a, s);
       if (g_use_glds == 7) return launch_gemm8<2, 0>(k, a, s);
       if (g_use_glds == 8) return launch_gemm8<0, -1>(k, a, s);
-      if (g_use_glds == 10) {  // persistent variant (experimental: the epilogue's ordinary loads make hipcc
-                               // drain the prefetch with vmcnt(0) at every K-step; slower until fixed)
-        if (a->act == OCTSAM_ACT_RELU) return launch_gemm8p<OCTSAM_ACT_RELU>(k, a, s);
-        if (a->act == OCTSAM_ACT_GELU) return launch_gemm8p<OCTSAM_ACT_GELU>(k, a, s);
-        return launch_gemm8p<0>(k, a, s);
+      // persistent variant: bias / activation epilogues (no residual or row map loads in the epilogue);
+      // fast path 11 forces the one-tile-per-workgroup kernel (A/B diagnostics)
+      const bool persist = a->R == nullptr && a->row_map == nullptr && a->N <= ph8::BIAS_MAX && g_use_glds != 11 &&
+                           (long long)a->M * a->lda * 2 < (1LL << 31) && (long long)a->N * a->ldb * 2 < (1LL << 31);
+      if (persist) {
+        // fast paths 12..15: persistent-kernel diagnostics (bit 0: relaxed waits after full-tile epilogues,
+        // bit 1: one tile per workgroup)
+        // (16: no epilogue stores, 17: every tile stores to tile 0)
+        const int dbg = g_use_glds >= 12 && g_use_glds <= 15 ? g_use_glds - 12
+                        : g_use_glds == 16 ? 4 : g_use_glds == 17 ? 8 : 0;
+        if (a->act == OCTSAM_ACT_RELU) return launch_gemm8p<OCTSAM_ACT_RELU>(k, a, s, dbg);
+        if (a->act == OCTSAM_ACT_GELU) return launch_gemm8p<OCTSAM_ACT_GELU>(k, a, s, dbg);
+        return launch_gemm8p<0>(k, a, s, dbg);
       }
       if (a->act == OCTSAM_ACT_RELU) return launch_gemm8<0, OCTSAM_ACT_RELU>(k, a, s);
       if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<0, OCTSAM_ACT_GELU>(k, a, s);

@@ -141,9 +141,10 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
     rm[::7] = -1
     rm = rm.to(cuda)
     outs = []
-    # 1: 8-phase kernel, one tile per workgroup (register epilogue; beta != 0 goes to the ring kernel), 10: persistent
-    # 8-phase, 8: 8-phase with the LDS-staged epilogue, 5: persistent ring kernel, 0: generic
-    for fast in (1, 10, 8, 5, 0):
+    # 1: default (a row map -> the 8-phase kernel, one tile per workgroup, register epilogue; beta != 0 goes to
+    # the ring kernel), 11: same, forced, 8: 8-phase with the LDS-staged epilogue, 5: persistent ring kernel,
+    # 0: generic
+    for fast in (1, 11, 8, 5, 0):
         lib.octsam_gemm_set_fast_path(fast | 256)  # 256: keep this shape off the small-problem path
         out = C0.clone()
         pout = None if pre is None else torch.zeros(Bt, M, N, device=cuda,
@@ -154,7 +155,7 @@ def test_gemm_fast_path_epilogues(cuda, c_f32, resid, beta, pre):
             kw.update(residual=R, stride_r=M * N)
         kernels.gemm(A, W, **kw)
         p8 = 2 if beta == 0.0 else 1
-        assert lib.octsam_gemm_last_path() == {1: p8, 10: p8, 8: p8, 5: 1, 0: 0}[fast]
+        assert lib.octsam_gemm_last_path() == {1: p8, 11: p8, 8: p8, 5: 1, 0: 0}[fast]
         outs.append((out, pout))
     lib.octsam_gemm_set_fast_path(1)
     keep = (rm >= 0).nonzero().flatten()
@@ -193,6 +194,43 @@ def test_gemm8_register_epilogue_act(cuda, act, M, N, K):
     pre = A.float() @ W.float().t() + bias
     ref = {0: pre, 1: F.relu(pre), 2: F.gelu(pre)}[act] + R.float()
     assert _rel(out, ref) < 8e-3
+
+
+@pytest.mark.parametrize("act", [0, 2])
+@pytest.mark.parametrize("M,N,K,Bt", [(39200, 2304, 768, 1), (4096, 768, 64, 1), (1100, 392, 128, 3),
+                                      (70000, 256, 192, 1), (20000, 3072, 768, 1)])
+@pytest.mark.parametrize("variant", ["bias", "nobias", "f32out", "pre"])
+def test_gemm8_persistent(cuda, act, M, N, K, Bt, variant):
+    """Persistent 8-phase kernel (bias from LDS, epilogue overlapped with the next tile's prefetch, relaxed
+    waits after full e16 tiles): several tiles per workgroup, K = 64 (one K-step per tile), ragged M/N,
+    batch strides, fp32 output and a pre-activation copy (conservative waits) against torch fp32 and the
+    one-tile-per-workgroup kernel."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + act + len(variant))
+    A = torch.randn(Bt, M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(Bt, N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = None if variant == "nobias" else torch.randn(N, generator=g).to(cuda)
+    cdt = torch.float32 if variant == "f32out" else torch.bfloat16
+    outs = []
+    for fast in (1, 11):
+        lib.octsam_gemm_set_fast_path(fast | 256)
+        out = torch.full((Bt, M, N), float("nan"), device=cuda, dtype=cdt)
+        pout = torch.zeros(Bt, M, N, device=cuda, dtype=torch.bfloat16) if variant == "pre" else None
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c=M * N,
+                     bias=bias, act=act, pre_out=pout)
+        assert lib.octsam_gemm_last_path() == 2
+        outs.append((out, pout))
+    lib.octsam_gemm_set_fast_path(1)
+    pre = torch.bmm(A.float(), W.float().transpose(1, 2)) + (bias if bias is not None else 0.0)
+    ref = F.gelu(pre) if act == 2 else pre
+    tol = 1e-5 if variant == "f32out" else 8e-3
+    for out, pout in outs:
+        assert not torch.isnan(out).any()
+        assert _rel(out, ref) < tol
+        if pout is not None:
+            assert _rel(pout, pre) < 8e-3
+    assert torch.equal(outs[0][0], outs[1][0])  # same MFMA order, same epilogue arithmetic
 
 
 @pytest.mark.parametrize("a_mode,b_mode", [(1, 0), (0, 1), (1, 1)])
