@@ -1249,6 +1249,23 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
         TR ? mma16(BF[ni][kb], af[mi][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0) \
            : mma16(af[mi][kb], BF[ni][kb], acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
+// first K-step of a tile: the kb = 0 MFMAs take an inline-constant zero accumulator (no per-tile zeroing of
+// the 128 accumulator registers)
+#define PH8_MFMA_QUAD_Z(MH, NH, BF)                                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                                        \
+  _Pragma("unroll") for (int kb = 0; kb < 2; ++kb)                                                     \
+  _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                                     \
+  _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                                                     \
+    acc[(MH) * 4 + mi][(NH) * 2 + ni] =                                                                 \
+        TR ? mma16(BF[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0) \
+           : mma16(af[mi][kb], BF[ni][kb], kb == 0 ? (f32x4)0.0f : acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+#define PH8_MFMA_QUAD_F(MH, NH, BF, FIRST) \
+  if (FIRST) {                             \
+    PH8_MFMA_QUAD_Z(MH, NH, BF)            \
+  } else {                                 \
+    PH8_MFMA_QUAD(MH, NH, BF)              \
+  }
 
 // EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA).
 // FE: 0 = general register epilogue, 1 = lean buffer-store epilogue, 2 = lean with an e16 residual (both need
@@ -1272,11 +1289,13 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   const e16* B = (const e16*)p.B + bz * p.sB;
   const int nk = p.K / 64;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][4];  // written by the first K-step's zero-accumulator MFMAs
+  if (DBG == 2 || p.K < 64) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+  }
   e16x8 af[4][2], b0[2][2], b1[2][2];
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
 
@@ -1315,7 +1334,7 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(0, 0, b0)
+    PH8_MFMA_QUAD_F(0, 0, b0, t == 0)
     raw_barrier();
     // ---- phase 1: Q(0,1) — B-n1
 #pragma unroll
@@ -1326,7 +1345,7 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(0, 1, b1)
+    PH8_MFMA_QUAD_F(0, 1, b1, t == 0)
     raw_barrier();
     // ---- phase 2: Q(1,0) — A-hi; restage A-lo, B-n0 of K-tile t+2
     if (h2) {
@@ -1339,14 +1358,14 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
       for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + 64 + mi * 16, kb * 4 + kq);
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(1, 0, b0)
+    PH8_MFMA_QUAD_F(1, 0, b0, t == 0)
     raw_barrier();
     // ---- phase 3: Q(1,1); restage B-n1 of K-tile t+2; retire A-lo, B-n0 of K-tile t+1
     if (h2) ph8::load_region(p, A, B, 3, row0, col0, (t + 2) * 64, cur, wave, lane);
     if (h2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else if (h1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     raw_barrier();
-    PH8_MFMA_QUAD(1, 1, b1)
+    PH8_MFMA_QUAD_F(1, 1, b1, t == 0)
     raw_barrier();
   }
   if (wr == 0) raw_barrier();  // balance the stagger
@@ -1470,11 +1489,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
   GemmK pe = p;          // the epilogue's view (diagnostics: 4 = no stores, 8 = every tile stores to tile 0)
   if (dbg & 4) pe.M = 0;
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+  f32x4 acc[8][4];  // written by each tile's first K-step (zero-accumulator MFMAs); K >= 64 host-checked
   e16x8 af[4][2], b0[2][2], b1[2][2];
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
 
@@ -1517,6 +1532,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
     const char* cb = cur + 32768;
     const bool h1 = g + 1 < G, h2 = g + 2 < G;
     const bool rx1 = relax_epi && since == 1, rx0 = relax_epi && since <= 2;
+    const bool first_k = cc.kt == 0;
     // ---- phase 0: Q(0,0) — A-lo, B-n0
     if (h1) issue(c1, 1, nxt);
 #pragma unroll
@@ -1530,7 +1546,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(0, 0, b0)
+    PH8_MFMA_QUAD_F(0, 0, b0, first_k)
     raw_barrier();
     // ---- phase 1: Q(0,1) — B-n1
 #pragma unroll
@@ -1541,7 +1557,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(0, 1, b1)
+    PH8_MFMA_QUAD_F(0, 1, b1, first_k)
     raw_barrier();
     // ---- phase 2: Q(1,0) — A-hi; restage A-lo, B-n0 of step g+2
     if (h2) {
@@ -1554,14 +1570,14 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
       for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + 64 + mi * 16, kb * 4 + kq);
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    PH8_MFMA_QUAD(1, 0, b0)
+    PH8_MFMA_QUAD_F(1, 0, b0, first_k)
     raw_barrier();
     // ---- phase 3: Q(1,1); restage B-n1 of step g+2; retire A-lo, B-n0 of step g+1
     if (h2) issue(c2, 3, cur);
     if (h2) ph8::vm_wait<10>(rx1);
     else if (h1) ph8::vm_wait<4>(rx1);
     raw_barrier();
-    PH8_MFMA_QUAD(1, 1, b1)
+    PH8_MFMA_QUAD_F(1, 1, b1, first_k)
     raw_barrier();
     ++since;
     if (++cc.kt == nk) {  // last K-step of tile cc.i: epilogue while steps g+1, g+2 load
@@ -1574,10 +1590,6 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
         ph8::epilogue_reg<EPI, 0, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
         ph8::epilogue_reg<EPI, 4, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
       }
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4)0.0f;
       relax_epi = relax_ok && cc.row0 + 256 <= p.M && cc.col0 + 256 <= p.N;
       since = 1;
       cc = c1;  // (c1 is tile cc.i + 1 at K-tile 0 here)
