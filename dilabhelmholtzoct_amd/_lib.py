@@ -34,7 +34,7 @@ class GemmArgs(ctypes.Structure):
         ("c_f32", c_int32), ("r_f32", c_int32), ("pre_f32", c_int32), ("conv_c", c_int32),
         ("a2_rows", c_int32), ("b2_rows", c_int32),
         ("a_blk", c_int32), ("a_rep", c_int32), ("b_blk", c_int32), ("b_rep", c_int32),
-        ("r_blk", c_int32), ("r_rep", c_int32), ("k_total", c_int32),
+        ("r_blk", c_int32), ("r_rep", c_int32), ("k_total", c_int32), ("c_rows", c_int32),
     ]
 
 

@@ -101,7 +101,8 @@ struct GemmK {
   int conv_c;  // channels for conv3x3 mode
   int tiles_m, tiles_n;
   int k_total;  // split-K over k-major operands: rows >= k_total (counted from batch 0) read as zero
-  int fast_epi;  // 8-phase kernels: e16 C (+ optional e16 residual) without row map / C_pre, 32-bit offsets
+  int fast_epi;  // 8-phase kernels: lean epilogue kind (0 = general; else 1 + FE bits, see epilogue_fast)
+  int c_rows;    // rows of C (and R) when a row map scatters the output (fast epilogue range)
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -1145,21 +1146,43 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
   }
 }
 
-// Lean register epilogue for a tile whose 256 columns are all inside N, e16 C, no row map / C_pre: C (and an
-// e16 residual) go through buffer descriptors that start at the wave's first row and end at row M, so rows
-// past M are dropped (stores) or read as zero (residual) by the hardware range check, and every store is
-// one voffset add + buffer_store_dwordx4. RES: e16 residual; BIAS_LDS: bias read from LDS (persistent
-// kernel), else from global. Host guarantees M * ldc * 2 and M * ldr * 2 < 2^31 (fast_epi).
-template <int ACT, bool RES, bool BIAS_LDS, int MI0 = 0, int NMI = 8>
+// Lean register epilogue for a tile whose 256 columns are all inside N (no C_pre): C and the residual go
+// through buffer descriptors, so every store is one voffset add + buffer_store_dwordx4 and the hardware
+// range check takes the row bounds — rows past M are dropped (stores) / read as zero (residual).
+//   FE bits (FE = 1 + bits): 1 fp32 C (else e16), 2 residual of C's type and layout (ldr, stride_r), 4 row map
+//   (output row row_map[m], -1 = dropped; the descriptors then span the whole C / R, row m's offset is
+//   row_map[m] * ld, a dropped row gets an offset past the range).
+// BIAS_LDS: bias read from LDS (persistent kernel), else from global. Host guarantees (fast_epi) that every
+// byte offset fits 31 bits: M * ld * esize without a row map, c_rows * ld * esize with one.
+template <int ACT, int FE, bool BIAS_LDS, int MI0 = 0, int NMI = 8>
 __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0,
                                               int lane, const float* lds_bias = nullptr) {
+  constexpr bool CF32 = ((FE - 1) & 1) != 0, RES = ((FE - 1) & 2) != 0, RMAP = ((FE - 1) & 4) != 0;
+  constexpr int ES = CF32 ? 4 : 2;
   const int q = lane >> 4;
   const int cofs = 16 * (q & 1) + 8 * (q >> 1);
+  // descriptor origin / extent and each lane's row offsets (bytes)
+  const long long c_origin = RMAP ? bz * p.sC + col0 : bz * p.sC + (long long)row0 * p.ldc + col0;
+  const long long r_origin = RMAP ? bz * p.sR + col0 : bz * p.sR + (long long)row0 * p.ldr + col0;
   const int rows_left = max(0, p.M - row0);
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((e16*)p.C + bz * p.sC + (long long)row0 * p.ldc + col0), (short)0, (int)(rows_left * p.ldc * 2),
-      0x00020000);
-  const uint32_t vb = (uint32_t)(((lane & 15) * p.ldc + cofs) * 2);
+  const int c_bytes = RMAP ? p.c_rows * (int)p.ldc * ES : rows_left * (int)p.ldc * ES;
+  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.C + c_origin * ES), (short)0, c_bytes, 0x00020000);
+  uint32_t crow[NMI], rrow[NMI];
+#pragma unroll
+  for (int j = 0; j < NMI; ++j) {
+    const int rl = 16 * (MI0 + j) + (lane & 15);  // row within the wave tile
+    if constexpr (RMAP) {
+      const int m = row0 + rl;
+      const int om = m < p.M ? p.row_map[m] : -1;
+      crow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldc * ES) : 0x80000000u;
+      rrow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldr * ES) : 0x80000000u;
+    } else {
+      crow[j] = (uint32_t)(rl * (int)p.ldc * ES);
+      rrow[j] = (uint32_t)(rl * (int)p.ldr * ES);
+    }
+  }
   float v[NMI][2][8];
 #pragma unroll
   for (int j = 0; j < NMI; ++j)
@@ -1209,32 +1232,56 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
 #pragma unroll
       for (int e = 0; e < 8; ++e) bv[pr][e] = 0.0f;
   }
-  u32x4 raw[RES ? NMI : 1][2];
+  const uint32_t cl = (uint32_t)(cofs * ES);
+  float res[RES ? NMI : 1][2][8];
   if constexpr (RES) {
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const e16*)p.R + bz * p.sR + (long long)row0 * p.ldr + col0), (short)0,
-        (int)(rows_left * p.ldr * 2), 0x00020000);
-    const uint32_t rb = (uint32_t)(((lane & 15) * p.ldr + cofs) * 2);
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.R + r_origin * ES), (short)0, r_bytes, 0x00020000);
 #pragma unroll
     for (int j = 0; j < NMI; ++j)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-        raw[j][pr] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, rb + (uint32_t)((16 * (MI0 + j) * p.ldr + 32 * pr) * 2), 0, 0));
+      for (int pr = 0; pr < 2; ++pr) {
+        const uint32_t o = rrow[j] + cl + (uint32_t)(32 * pr * ES);
+        if constexpr (CF32) {
+          const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
+          const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o + 16, 0, 0));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            res[j][pr][e] = a[e];
+            res[j][pr][4 + e] = b[e];
+          }
+        } else {
+          const u32x4 w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            res[j][pr][2 * e] = lo16f(w[e]);
+            res[j][pr][2 * e + 1] = hi16f(w[e]);
+          }
+        }
+      }
   }
 #pragma unroll
   for (int j = 0; j < NMI; ++j)
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
-      e16x8 o;
+      float o8[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float t = act_apply<ACT>(v[j][pr][e] * p.alpha + bv[pr][e]);
-        if constexpr (RES) t += (e & 1) ? hi16f(raw[j][pr][e >> 1]) : lo16f(raw[j][pr][e >> 1]);
-        o[e] = (e16)t;
+        if constexpr (RES) t += res[j][pr][e];
+        o8[e] = t;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc,
-                                             vb + (uint32_t)((16 * (MI0 + j) * p.ldc + 32 * pr) * 2), 0, 0);
+      const uint32_t o = crow[j] + cl + (uint32_t)(32 * pr * ES);
+      if constexpr (CF32) {
+        const f32x4 a = {o8[0], o8[1], o8[2], o8[3]}, b = {o8[4], o8[5], o8[6], o8[7]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rc, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rc, o + 16, 0, 0);
+      } else {
+        e16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (e16)o8[e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), rc, o, 0, 0);
+      }
     }
 }
 }  // namespace ph8
@@ -1268,8 +1315,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
   }
 
 // EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA).
-// FE: 0 = general register epilogue, 1 = lean buffer-store epilogue, 2 = lean with an e16 residual (both need
-// N % 256 == 0 and fast_epi; one epilogue per instantiation keeps the register allocation spill-free)
+// FE: 0 = general register epilogue, else the lean buffer epilogue of that kind (epilogue_fast; needs
+// N % 256 == 0; one epilogue per instantiation keeps the register allocation spill-free)
 template <int DBG, int EPI, int FE = 0>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   constexpr bool TR = EPI >= 0;
@@ -1380,11 +1427,11 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     return;
   }
   if constexpr (TR) {
-    if constexpr (FE == 2) {
-      ph8::epilogue_fast<EPI, true, false, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
-      ph8::epilogue_fast<EPI, true, false, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
-    } else if constexpr (FE == 1) {
-      ph8::epilogue_fast<EPI, false, false>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    if constexpr (FE == 1) {
+      ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    } else if constexpr (FE > 1) {  // halves: the residual / fp32 temporaries fit beside the accumulator
+      ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+      ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
     } else {
       ph8::epilogue_reg<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
     }
@@ -1413,8 +1460,16 @@ int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 
 template <int DBG, int EPI>
 int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
-  if (EPI >= 0 && DBG == 0 && k.fast_epi && a->N % 256 == 0)
-    return a->R ? launch_gemm8_fe<DBG, EPI, 2>(k, a, s) : launch_gemm8_fe<DBG, EPI, 1>(k, a, s);
+  if constexpr (EPI >= 0 && DBG == 0) {
+    if (a->N % 256 == 0) switch (k.fast_epi) {  // the kinds the encoder and decoder use
+        case 1: return launch_gemm8_fe<DBG, EPI, 1>(k, a, s);  // e16 C
+        case 2: return launch_gemm8_fe<DBG, EPI, 2>(k, a, s);  // fp32 C
+        case 3: return launch_gemm8_fe<DBG, EPI, 3>(k, a, s);  // e16 C + e16 residual
+        case 4: return launch_gemm8_fe<DBG, EPI, 4>(k, a, s);  // fp32 C + fp32 residual
+        case 8: return launch_gemm8_fe<DBG, EPI, 8>(k, a, s);  // fp32 C + fp32 residual, row map
+        default: break;
+      }
+  }
   return launch_gemm8_fe<DBG, EPI, 0>(k, a, s);
 }
 
@@ -1583,9 +1638,9 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
     if (++cc.kt == nk) {  // last K-step of tile cc.i: epilogue while steps g+1, g+2 load
       const int ebz = (dbg & 8) ? 0 : (first + cc.i * stride) / per_batch;
       const int er0 = ((dbg & 8) ? 0 : cc.row0) + wr * 128, ec0 = ((dbg & 8) ? 0 : cc.col0) + wc * 64;
-      if constexpr (FE == 1) {
-        ph8::epilogue_fast<EPI, false, true, 0, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
-        ph8::epilogue_fast<EPI, false, true, 4, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
+      if constexpr (FE != 0) {
+        ph8::epilogue_fast<EPI, FE, true, 0, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
+        ph8::epilogue_fast<EPI, FE, true, 4, 4>(pe, acc, ebz, er0, ec0, lane, lbias);
       } else {
         ph8::epilogue_reg<EPI, 0, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
         ph8::epilogue_reg<EPI, 4, 4, true>(pe, acc, ebz, er0, ec0, lane, lbias);
@@ -1624,7 +1679,8 @@ int launch_gemm8p_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, 
 }
 template <int EPI>
 int launch_gemm8p(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, int dbg) {
-  if (k.fast_epi && a->N % 256 == 0) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
+  if (a->N % 256 == 0 && k.fast_epi == 1) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
+  if (a->N % 256 == 0 && k.fast_epi == 2) return launch_gemm8p_fe<EPI, 2>(k, a, s, dbg);
   return launch_gemm8p_fe<EPI, 0>(k, a, s, dbg);
 }
 
@@ -1754,10 +1810,19 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
   k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
   k.k_total = a->k_total;
-  k.fast_epi = !a->c_f32 && a->C_pre == nullptr && a->row_map == nullptr && (a->ldc & 7) == 0 &&
-               ((uintptr_t)a->C & 15) == 0 && (long long)a->M * a->ldc * 2 < (1LL << 31) &&
-               (a->R == nullptr || (!a->r_f32 && a->r_blk == 0 && (a->ldr & 7) == 0 && ((uintptr_t)a->R & 15) == 0 &&
-                                    (long long)a->M * a->ldr * 2 < (1LL << 31)));
+  {  // lean epilogue kind (epilogue_fast): no C_pre; a residual must have C's type, no broadcast (r_blk)
+    const int es = a->c_f32 ? 4 : 2;
+    const bool res_ok = a->R == nullptr || (a->r_f32 == a->c_f32 && a->r_blk == 0 && (a->ldr & 7) == 0 &&
+                                            ((uintptr_t)a->R & 15) == 0);
+    const long long rows = a->row_map ? (long long)a->c_rows : (long long)a->M;
+    const bool range_ok = rows > 0 && rows * a->ldc * es < (1LL << 31) &&
+                          (a->R == nullptr || rows * a->ldr * es < (1LL << 31));
+    k.fast_epi = (a->C_pre == nullptr && (a->ldc & 7) == 0 && ((uintptr_t)a->C & 15) == 0 && res_ok && range_ok)
+                     ? 1 + (a->c_f32 ? 1 : 0) + (a->R ? 2 : 0) + (a->row_map ? 4 : 0)
+                     : 0;
+    k.c_rows = a->c_rows;
+    if (g_use_glds == 18) k.fast_epi = 0;  // diagnostics / parity: the general register epilogue
+  }
   OCTSAM_CHECK_ARG(a->k_total == 0 || (a->a_mode == 1 && a->b_mode == 1 && a->k_total <= (long long)a->K * a->batch &&
                                        a->k_total > (long long)a->K * (a->batch - 1)),
                    "octsam_gemm: k_total needs a_mode = b_mode = 1 and (batch-1)*K < k_total <= batch*K");

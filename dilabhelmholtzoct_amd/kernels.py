@@ -56,7 +56,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         r_f32=int(residual is not None and residual.dtype == torch.float32),
         pre_f32=int(pre_out is not None and pre_out.dtype == torch.float32),
         conv_c=conv_c, a2_rows=a2_rows, b2_rows=b2_rows, a_blk=a_remap[0], a_rep=a_remap[1],
-        b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total)
+        b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
+        c_rows=min(out.numel() // ldc, 2 ** 31 - 1) if row_map is not None else 0)
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 9
+#define OCTSAM_ABI_VERSION 10
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -75,6 +75,9 @@ typedef struct octsam_gemm_args {
   /* k-major A and B (a_mode = b_mode = 1) batched as split-K over one [k_total][*] operand pair:
      batch b covers rows [b*K, (b+1)*K) and rows >= k_total read as zero (0 = no tail). */
   int32_t k_total;
+  /* rows of C (and R) when row_map scatters the output; lets the 256x256 kernels use their lean epilogue
+     (byte offsets range-checked against c_rows * ldc); 0 = unknown (general epilogue) */
+  int32_t c_rows;
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);

@@ -233,6 +233,56 @@ def test_gemm8_persistent(cuda, act, M, N, K, Bt, variant):
     assert torch.equal(outs[0][0], outs[1][0])  # same MFMA order, same epilogue arithmetic
 
 
+@pytest.mark.parametrize("kind", ["e16", "f32", "e16_res", "f32_res", "f32_res_rowmap"])
+@pytest.mark.parametrize("act", [0, 2])
+def test_gemm8_lean_epilogue_kinds(cuda, kind, act):
+    """The lean buffer-descriptor epilogue (N % 256 == 0) for every output kind the encoder uses — e16 or fp32
+    C, a residual of C's type read in place, a row map with dropped rows (windowed attention's projection) —
+    against torch fp32 and against the general register epilogue (fast path 18), ragged M, batch strides."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    rowmap = kind.endswith("rowmap")
+    Bt = 1 if rowmap else 2
+    M, N, K = 1100, 512, 192
+    g = torch.Generator().manual_seed(len(kind) * 10 + act)
+    A = torch.randn(Bt, M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(Bt, N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    cdt = torch.float32 if kind.startswith("f32") else torch.bfloat16
+    Mc = 1500 if rowmap else M  # rows of C (the row map scatters into a larger output)
+    C0 = torch.randn(Bt, Mc, N, generator=g).to(cuda, cdt)
+    rm = None
+    if rowmap:
+        rm = torch.randperm(Mc, generator=g)[:M].to(torch.int32)
+        rm[::5] = -1
+        rm = rm.to(cuda)
+    outs = []
+    for fast in (1, 18):
+        lib.octsam_gemm_set_fast_path(fast | 256)
+        out = C0.clone()
+        kw = dict(M=M, N=N, K=K, out=out, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c=Mc * N, bias=bias,
+                  act=act, row_map=rm)
+        if "res" in kind:
+            kw.update(residual=out, stride_r=Mc * N)
+        kernels.gemm(A, W, **kw)
+        assert lib.octsam_gemm_last_path() == 2
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    pre = torch.bmm(A.float(), W.float().transpose(1, 2)) + bias
+    y = F.gelu(pre) if act == 2 else pre
+    keep = torch.arange(M, device=cuda) if rm is None else (rm >= 0).nonzero().flatten()
+    dst = keep if rm is None else rm[keep].long()
+    ref = C0.float().clone()
+    ref[:, dst] = y[:, keep] + (C0.float()[:, dst] if "res" in kind else 0.0)
+    tol = 1e-5 if cdt == torch.float32 else 8e-3
+    for out in outs:
+        assert _rel(out.float(), ref) < tol
+        untouched = torch.ones(Mc, dtype=torch.bool, device=cuda)
+        untouched[dst] = False
+        assert torch.equal(out[:, untouched], C0[:, untouched])
+    assert _rel(outs[0].float(), outs[1].float()) < 1e-6 if cdt == torch.float32 else torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("a_mode,b_mode", [(1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("shape", [(1104, 392, 192, 2), (256, 256, 128, 64), (128, 264, 64, 40)])
 def test_gemm_fast_path_kmajor(cuda, a_mode, b_mode, shape):
