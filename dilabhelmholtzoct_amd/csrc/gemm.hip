@@ -1146,27 +1146,30 @@ __device__ __forceinline__ void epilogue_reg(const GemmK& p, f32x4 (&acc)[8][4],
   }
 }
 
-// Lean register epilogue for a tile whose 256 columns are all inside N (no C_pre): C and the residual go
-// through buffer descriptors, so every store is one voffset add + buffer_store_dwordx4 and the hardware
-// range check takes the row bounds — rows past M are dropped (stores) / read as zero (residual).
-//   FE bits (FE = 1 + bits): 1 fp32 C (else e16), 2 residual of C's type and layout (ldr, stride_r), 4 row map
-//   (output row row_map[m], -1 = dropped; the descriptors then span the whole C / R, row m's offset is
-//   row_map[m] * ld, a dropped row gets an offset past the range).
+// Lean register epilogue (no C_pre, N % 8 == 0): C and the residual go through buffer descriptors, so every
+// store is one voffset add + buffer_store_dwordx4 and the hardware range check takes the row bounds — rows
+// past M are dropped (stores) / read as zero (residual); columns past N (a ragged last column tile) are
+// masked per lane.
+//   FE bits (FE = 1 + bits): 1 fp32 C (else e16), 2 residual of C's type (ldr, stride_r), 4 row map (output
+//   row row_map[m], -1 = dropped; the descriptors then span the whole C / R, row m's offset is
+//   row_map[m] * ld, a dropped row gets an offset past the range), 8 residual row remap (r_blk, r_rep:
+//   residual row = remap(m), a broadcast addend such as the decoder's per-prompt positional projection).
 // BIAS_LDS: bias read from LDS (persistent kernel), else from global. Host guarantees (fast_epi) that every
 // byte offset fits 31 bits: M * ld * esize without a row map, c_rows * ld * esize with one.
 template <int ACT, int FE, bool BIAS_LDS, int MI0 = 0, int NMI = 8>
 __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0, int col0,
                                               int lane, const float* lds_bias = nullptr) {
   constexpr bool CF32 = ((FE - 1) & 1) != 0, RES = ((FE - 1) & 2) != 0, RMAP = ((FE - 1) & 4) != 0;
+  constexpr bool RREMAP = ((FE - 1) & 8) != 0;
   constexpr int ES = CF32 ? 4 : 2;
   const int q = lane >> 4;
   const int cofs = 16 * (q & 1) + 8 * (q >> 1);
   // descriptor origin / extent and each lane's row offsets (bytes)
   const long long c_origin = RMAP ? bz * p.sC + col0 : bz * p.sC + (long long)row0 * p.ldc + col0;
-  const long long r_origin = RMAP ? bz * p.sR + col0 : bz * p.sR + (long long)row0 * p.ldr + col0;
+  const long long r_origin = (RMAP || RREMAP) ? bz * p.sR + col0 : bz * p.sR + (long long)row0 * p.ldr + col0;
   const int rows_left = max(0, p.M - row0);
   const int c_bytes = RMAP ? p.c_rows * (int)p.ldc * ES : rows_left * (int)p.ldc * ES;
-  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
+  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : RREMAP ? p.M * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.C + c_origin * ES), (short)0, c_bytes, 0x00020000);
   uint32_t crow[NMI], rrow[NMI];
@@ -1180,9 +1183,14 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
       rrow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldr * ES) : 0x80000000u;
     } else {
       crow[j] = (uint32_t)(rl * (int)p.ldc * ES);
-      rrow[j] = (uint32_t)(rl * (int)p.ldr * ES);
+      rrow[j] = RREMAP ? (uint32_t)((int)remap(row0 + rl, p.r_blk, p.r_rep) * (int)p.ldr * ES)
+                       : (uint32_t)(rl * (int)p.ldr * ES);
+      if (RREMAP && row0 + rl >= p.M) rrow[j] = 0x80000000u;
     }
   }
+  bool colok[2];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) colok[pr] = col0 + 32 * pr + cofs < p.N;
   float v[NMI][2][8];
 #pragma unroll
   for (int j = 0; j < NMI; ++j)
@@ -1203,7 +1211,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
     f32x4 t[2][2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
-      const int n = col0 + 32 * pr + cofs;
+      const int n = colok[pr] ? col0 + 32 * pr + cofs : 0;  // (columns past N: any in-range bias, never stored)
       if constexpr (BIAS_LDS) {
         // inline asm: hipcc would put a vmcnt(0) (the in-flight LDS-DMA prefetch) in front of an ordinary
         // LDS load; the bias region is never a DMA target
@@ -1271,7 +1279,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
         if constexpr (RES) t += res[j][pr][e];
         o8[e] = t;
       }
-      const uint32_t o = crow[j] + cl + (uint32_t)(32 * pr * ES);
+      // a column chunk past N is sent past the descriptor's range (dropped) instead of branching
+      const uint32_t o = colok[pr] ? crow[j] + cl + (uint32_t)(32 * pr * ES) : 0x80000000u;
       if constexpr (CF32) {
         const f32x4 a = {o8[0], o8[1], o8[2], o8[3]}, b = {o8[4], o8[5], o8[6], o8[7]};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rc, o, 0, 0);
@@ -1461,14 +1470,15 @@ int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 template <int DBG, int EPI>
 int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   if constexpr (EPI >= 0 && DBG == 0) {
-    if (a->N % 256 == 0) switch (k.fast_epi) {  // the kinds the encoder and decoder use
-        case 1: return launch_gemm8_fe<DBG, EPI, 1>(k, a, s);  // e16 C
-        case 2: return launch_gemm8_fe<DBG, EPI, 2>(k, a, s);  // fp32 C
-        case 3: return launch_gemm8_fe<DBG, EPI, 3>(k, a, s);  // e16 C + e16 residual
-        case 4: return launch_gemm8_fe<DBG, EPI, 4>(k, a, s);  // fp32 C + fp32 residual
-        case 8: return launch_gemm8_fe<DBG, EPI, 8>(k, a, s);  // fp32 C + fp32 residual, row map
-        default: break;
-      }
+    switch (k.fast_epi) {  // the kinds the encoder and decoder use
+      case 1: return launch_gemm8_fe<DBG, EPI, 1>(k, a, s);    // e16 C
+      case 2: return launch_gemm8_fe<DBG, EPI, 2>(k, a, s);    // fp32 C
+      case 3: return launch_gemm8_fe<DBG, EPI, 3>(k, a, s);    // e16 C + e16 residual
+      case 4: return launch_gemm8_fe<DBG, EPI, 4>(k, a, s);    // fp32 C + fp32 residual
+      case 8: return launch_gemm8_fe<DBG, EPI, 8>(k, a, s);    // fp32 C + fp32 residual, row map
+      case 11: return launch_gemm8_fe<DBG, EPI, 11>(k, a, s);  // e16 C + broadcast e16 residual
+      default: break;
+    }
   }
   return launch_gemm8_fe<DBG, EPI, 0>(k, a, s);
 }
@@ -1679,8 +1689,10 @@ int launch_gemm8p_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, 
 }
 template <int EPI>
 int launch_gemm8p(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, int dbg) {
-  if (a->N % 256 == 0 && k.fast_epi == 1) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
-  if (a->N % 256 == 0 && k.fast_epi == 2) return launch_gemm8p_fe<EPI, 2>(k, a, s, dbg);
+  if (k.fast_epi == 1) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
+  // (fp32 output + GELU would spill in this kernel: general epilogue)
+  if constexpr (EPI != OCTSAM_ACT_GELU)
+    if (k.fast_epi == 2) return launch_gemm8p_fe<EPI, 2>(k, a, s, dbg);
   return launch_gemm8p_fe<EPI, 0>(k, a, s, dbg);
 }
 
@@ -1812,13 +1824,14 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   k.k_total = a->k_total;
   {  // lean epilogue kind (epilogue_fast): no C_pre; a residual must have C's type, no broadcast (r_blk)
     const int es = a->c_f32 ? 4 : 2;
-    const bool res_ok = a->R == nullptr || (a->r_f32 == a->c_f32 && a->r_blk == 0 && (a->ldr & 7) == 0 &&
-                                            ((uintptr_t)a->R & 15) == 0);
+    const bool res_ok = a->R == nullptr || (a->r_f32 == a->c_f32 && (a->r_blk == 0 || a->row_map == nullptr) &&
+                                            (a->ldr & 7) == 0 && ((uintptr_t)a->R & 15) == 0);
     const long long rows = a->row_map ? (long long)a->c_rows : (long long)a->M;
     const bool range_ok = rows > 0 && rows * a->ldc * es < (1LL << 31) &&
                           (a->R == nullptr || rows * a->ldr * es < (1LL << 31));
     k.fast_epi = (a->C_pre == nullptr && (a->ldc & 7) == 0 && ((uintptr_t)a->C & 15) == 0 && res_ok && range_ok)
-                     ? 1 + (a->c_f32 ? 1 : 0) + (a->R ? 2 : 0) + (a->row_map ? 4 : 0)
+                     ? 1 + (a->c_f32 ? 1 : 0) + (a->R ? 2 : 0) + (a->row_map ? 4 : 0) +
+                           (a->R && a->r_blk > 0 ? 8 : 0)
                      : 0;
     k.c_rows = a->c_rows;
     if (g_use_glds == 18) k.fast_epi = 0;  // diagnostics / parity: the general register epilogue

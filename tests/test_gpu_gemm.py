@@ -233,17 +233,20 @@ def test_gemm8_persistent(cuda, act, M, N, K, Bt, variant):
     assert torch.equal(outs[0][0], outs[1][0])  # same MFMA order, same epilogue arithmetic
 
 
-@pytest.mark.parametrize("kind", ["e16", "f32", "e16_res", "f32_res", "f32_res_rowmap"])
+@pytest.mark.parametrize("kind", ["e16", "f32", "e16_res", "f32_res", "f32_res_rowmap", "e16_bres"])
 @pytest.mark.parametrize("act", [0, 2])
-def test_gemm8_lean_epilogue_kinds(cuda, kind, act):
-    """The lean buffer-descriptor epilogue (N % 256 == 0) for every output kind the encoder uses — e16 or fp32
-    C, a residual of C's type read in place, a row map with dropped rows (windowed attention's projection) —
-    against torch fp32 and against the general register epilogue (fast path 18), ragged M, batch strides."""
+@pytest.mark.parametrize("N", [512, 392])
+def test_gemm8_lean_epilogue_kinds(cuda, kind, act, N):
+    """The lean buffer-descriptor epilogue for every output kind the encoder and decoder use — e16 or fp32 C,
+    a residual of C's type read in place, a row map with dropped rows (windowed attention's projection), a
+    broadcast residual (r_remap: the decoder's per-prompt positional projection) — against torch fp32 and
+    against the general register epilogue (fast path 18): ragged M, a ragged last column tile, batch strides."""
     from dilabhelmholtzoct_amd import _lib, kernels
     lib = _lib.load()
     rowmap = kind.endswith("rowmap")
-    Bt = 1 if rowmap else 2
-    M, N, K = 1100, 512, 192
+    bres = kind.endswith("bres")
+    Bt = 1 if (rowmap or bres) else 2
+    M, K = 1100, 192
     g = torch.Generator().manual_seed(len(kind) * 10 + act)
     A = torch.randn(Bt, M, K, generator=g).to(cuda, torch.bfloat16)
     W = (torch.randn(Bt, N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
@@ -251,6 +254,7 @@ def test_gemm8_lean_epilogue_kinds(cuda, kind, act):
     cdt = torch.float32 if kind.startswith("f32") else torch.bfloat16
     Mc = 1500 if rowmap else M  # rows of C (the row map scatters into a larger output)
     C0 = torch.randn(Bt, Mc, N, generator=g).to(cuda, cdt)
+    P = torch.randn(100, N, generator=g).to(cuda, cdt) if bres else None
     rm = None
     if rowmap:
         rm = torch.randperm(Mc, generator=g)[:M].to(torch.int32)
@@ -262,7 +266,9 @@ def test_gemm8_lean_epilogue_kinds(cuda, kind, act):
         out = C0.clone()
         kw = dict(M=M, N=N, K=K, out=out, batch=Bt, stride_a=M * K, stride_b=N * K, stride_c=Mc * N, bias=bias,
                   act=act, row_map=rm)
-        if "res" in kind:
+        if bres:
+            kw.update(residual=P, r_remap=(100, 11))  # residual row = m % 100 (M = 100 * 11)
+        elif "res" in kind:
             kw.update(residual=out, stride_r=Mc * N)
         kernels.gemm(A, W, **kw)
         assert lib.octsam_gemm_last_path() == 2
@@ -273,7 +279,10 @@ def test_gemm8_lean_epilogue_kinds(cuda, kind, act):
     keep = torch.arange(M, device=cuda) if rm is None else (rm >= 0).nonzero().flatten()
     dst = keep if rm is None else rm[keep].long()
     ref = C0.float().clone()
-    ref[:, dst] = y[:, keep] + (C0.float()[:, dst] if "res" in kind else 0.0)
+    if bres:
+        ref[:, dst] = y[:, keep] + P.float()[torch.arange(M, device=cuda) % 100]
+    else:
+        ref[:, dst] = y[:, keep] + (C0.float()[:, dst] if "res" in kind else 0.0)
     tol = 1e-5 if cdt == torch.float32 else 8e-3
     for out in outs:
         assert _rel(out.float(), ref) < tol
