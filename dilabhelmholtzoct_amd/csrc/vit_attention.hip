@@ -57,6 +57,8 @@ template <> struct ET<f16> {
 
 constexpr int NW = 8, THR = NW * 64, NBUF = 3;
 constexpr float L2E = 1.4426950408889634f;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float max3f(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 template <int HD> struct Geo {
   static_assert(HD == 64 || HD == 80, "head_dim 64 or 80");
@@ -296,26 +298,30 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
     // tile = key image row kh: rel_h is one constant per lane (log2 units), so max and exponent take it
     // once per tile: p = exp2(c1 * acc + (rh - m)), one FMA + one exp per score
     const float rh = relh[tile * 32 + l32];
-    float mx = -INFINITY;
+    // max: 16 three-input maxima (scores are finite: the kernel is built without NaN canonicalisation, see
+    // Makefile); sum: packed adds
+    float mx = sacc[0][0];
 #pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) mx = fmaxf(mx, fmaxf(sacc[t2][r], sacc[t2][r + 1]));
+    for (int i = 1; i < 31; i += 2) mx = max3f(mx, sacc[i >> 4][i & 15], sacc[(i + 1) >> 4][(i + 1) & 15]);
+    mx = fmaxf(mx, sacc[1][15]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, fmaf(mx, c1, rh));
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     const float c = rh - m_new;
-    float ls = 0.0f;
+    f32x2 ls2 = {0.0f, 0.0f};
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], c1, c));
-        sacc[t2][r] = pv;
-        ls += pv;
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 x = {sacc[t2][r], sacc[t2][r + 1]};
+        const f32x2 y = x * c1 + c;  // v_pk_fma_f32
+        const f32x2 pv = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+        sacc[t2][r] = pv[0];
+        sacc[t2][r + 1] = pv[1];
+        ls2 += pv;  // v_pk_add_f32
       }
-    l_run = fmaf(l_run, alpha, ls);
+    l_run = fmaf(l_run, alpha, ls2[0] + ls2[1]);
     if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
 #pragma unroll
       for (int td = 0; td < G::NTD; ++td) acc_o[td] *= alpha;
