@@ -1169,7 +1169,9 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
   const long long r_origin = (RMAP || RREMAP) ? bz * p.sR + col0 : bz * p.sR + (long long)row0 * p.ldr + col0;
   const int rows_left = max(0, p.M - row0);
   const int c_bytes = RMAP ? p.c_rows * (int)p.ldc * ES : rows_left * (int)p.ldc * ES;
-  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : RREMAP ? p.M * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
+  // (a remapped residual has r_blk * ceil(M / (r_blk * r_rep)) stored rows: remap(m) < that for m < M)
+  const int r_rows = RREMAP ? p.r_blk * ((p.M - 1) / (p.r_blk * p.r_rep) + 1) : 0;
+  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : RREMAP ? r_rows * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.C + c_origin * ES), (short)0, c_bytes, 0x00020000);
   uint32_t crow[NMI], rrow[NMI];
@@ -1249,7 +1251,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
     for (int j = 0; j < NMI; ++j)
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
-        const uint32_t o = rrow[j] + cl + (uint32_t)(32 * pr * ES);
+        // (columns past N read as zero: their offset is sent past the range like the stores')
+        const uint32_t o = colok[pr] ? rrow[j] + cl + (uint32_t)(32 * pr * ES) : 0x80000000u;
         if constexpr (CF32) {
           const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
           const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o + 16, 0, 0));
