@@ -15,8 +15,6 @@ over prompts (octsam_group_sum) before the weight-gradient GEMM.
 """
 from __future__ import annotations
 
-import os
-
 from types import SimpleNamespace
 
 import torch
@@ -360,62 +358,13 @@ class MaskDecoder(nn.Module):
         ldy = O if ldy is None else ldy
         if dx_out is not None:
             self._dx(dy_b, w, M, dx_out, ldy=ldy, beta=dx_beta, ldc=ldc)
+        self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
         gb = self.G(bname) if bgroup is None else self._group(self.flat_grad, bgroup, 0)
         src = dy_b if db_src is None else db_src
-
-        def leaf():
-            self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
-            if ldy == O or db_src is not None:
-                K.colsum(src, M, O, gb)
-            else:
-                K.colsum(dy_b.view(M, ldy)[:, :O].contiguous(), M, O, gb)
-        return self._leaf(leaf, dy_b, x_b, x_add, src)
-
-    # ------------------------------------------------------------------ weight-gradient leaves
-    # Weight and bias gradients are leaves of the backward graph (only the optimizer reads them), so they run
-    # on a second stream beside the input-gradient chain, whose token-side kernels leave most of the chip
-    # idle. Each leaf waits for an event recorded on the main stream after its inputs were produced; its inputs
-    # are kept alive until the join at the end of the backward (the main stream's allocator must not hand
-    # their memory out again while the leaf stream may still read it), and a main-stream kernel that later
-    # writes a leaf input in place first waits for that leaf (_leaf returns its completion event).
-    leaf_overlap = os.environ.get("OCTSAM_LEAF_OVERLAP", "1") != "0"
-
-    def _leaf_begin(self, dev):
-        self._leaf_keep = []
-        self._leaf_stream = None
-        # events of the previous backward: every wait on them was behind that backward's join, which the
-        # current stream has passed by now
-        self._leaf_events = []
-        # graph capture only: the replay carries the fork/join as graph edges (eager cross-stream event waits
-        # stalled the queue in a multi-test process on this runtime)
-        if self.leaf_overlap and dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-            streams = self.__dict__.setdefault("_leaf_streams", {})
-            if dev not in streams:
-                streams[dev] = torch.cuda.Stream(device=dev)
-            self._leaf_stream = streams[dev]
-
-    def _leaf(self, fn, *keep):
-        side = getattr(self, "_leaf_stream", None)
-        if side is None:
-            fn()
-            return None
-        ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream())
-        side.wait_event(ready)
-        self._leaf_keep.extend(t for t in keep if t is not None)
-        with torch.cuda.stream(side):
-            fn()
-            done = torch.cuda.Event()
-            done.record(side)
-        self._leaf_events.extend((ready, done))  # alive until the work that waits on them has run
-        return done
-
-    def _leaf_end(self):
-        side = getattr(self, "_leaf_stream", None)
-        if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
-        self._leaf_keep = []
-        self._leaf_stream = None
+        if ldy == O or db_src is not None:
+            K.colsum(src, M, O, gb)
+        else:
+            K.colsum(dy_b.view(M, ldy)[:, :O].contiguous(), M, O, gb)
 
     def _ln(self, x, prefix, eps, rows, *, f32_out=True):
         w, b = self.Bf(prefix + ".weight"), self.Bf(prefix + ".bias")
@@ -610,7 +559,6 @@ class MaskDecoder(nn.Module):
         tr = "transformer."
         G = self.ensure_grad()
         G.zero_()
-        self._leaf_begin(dev)
         nsel = len(s.sel)
         dm = dmasks.reshape(P, nsel, 65536).contiguous().float()
         # ---- mask head + ConvT2 (+ GELU), fused: recomputes the ConvT2 product from up1
@@ -628,11 +576,8 @@ class MaskDecoder(nn.Module):
         # read-modify-written by each block's projection backward and read by LayerNorm4's backward per block
         dkeys = torch.empty(RL, C, device=dev, dtype=b16)
         K.gemm(dup1pre, self.W("upscale_conv1.weight"), M=RL, N=C, K=256, out=dkeys, b_mode=0)
-
-        def up1_leaf():
-            self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256)
-            K.colsum(dup1pre, RL * 4, 64, self.G("upscale_conv1.bias"))
-        self._leaf(up1_leaf, s.keys2_b, dup1pre)
+        self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256)
+        K.colsum(dup1pre, RL * 4, 64, self.G("upscale_conv1.bias"))
         # ---- hypernetwork MLP backward -> dq7
         dq7 = torch.zeros(R, C, device=dev, dtype=f32)
         dq7v = dq7.view(P, T, C)
@@ -664,11 +609,9 @@ class MaskDecoder(nn.Module):
         # d keys2 += [dK | dV] @ [Wk; Wv]
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
         self._dx(dKV, wkv, RL, dkeys, beta=1.0)
-        def fkv_leaf():
-            self._dw_pe(dKV, s.keys2_b, RL, self._group(self.flat_grad, [f + "k_proj.weight", f + "v_proj.weight"],
-                                                         C), CI, s.pe_b)
-            K.colsum(dKV, RL, 2 * CI, self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
-        self._leaf(fkv_leaf, dKV, s.keys2_b)
+        self._dw_pe(dKV, s.keys2_b, RL, self._group(self.flat_grad, [f + "k_proj.weight", f + "v_proj.weight"], C),
+                    CI, s.pe_b)
+        K.colsum(dKV, RL, 2 * CI, self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
         # ---- two-way blocks in reverse
         for li in reversed(range(cfg.num_hidden_layers)):
             ls = s.layers[li]
@@ -685,9 +628,7 @@ class MaskDecoder(nn.Module):
             dkeys_in = ds4_b if li > 0 else None
             # s4 = keys_in + i2t_out @ Wo^T + bo
             dio_b = torch.empty(RL, CI, device=dev, dtype=b16)
-            # (ds4_b is read by this projection's weight-gradient leaf and later accumulated into in place)
-            ds4_leaf = self._lin_bwd(ds4_b, ls.i2t_o_b, i2t + "out_proj.weight", i2t + "out_proj.bias", RL,
-                                     dx_out=dio_b)
+            self._lin_bwd(ds4_b, ls.i2t_o_b, i2t + "out_proj.weight", i2t + "out_proj.bias", RL, dx_out=dio_b)
             # i2t attention
             KQV = ls.KQV
             if li == 0:
@@ -733,26 +674,19 @@ class MaskDecoder(nn.Module):
                 K.group_sum(dKV0, dK_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 K.group_sum(dKV0[:, CI:], dV_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 K.group_sum(dQp, dQ_img, ld_in=CI, cols=CI, groups=B, nper=N, rows_per=L)
-                def img_leaf():
-                    self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), x_add=s.pe_b, x_add_rows=L)
-                    self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L)
-                    self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"))
-                    K.colsum(dK_img, Mi, CI, self.G(t2i + "k_proj.bias"))
-                    K.colsum(dQ_img, Mi, CI, self.G(i2t + "q_proj.bias"))
-                    K.colsum(dV_img, Mi, CI, self.G(t2i + "v_proj.bias"))
-                self._leaf(img_leaf, dK_img, dQ_img, dV_img, s.imgd_b, s.pe_b)
+                self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), x_add=s.pe_b, x_add_rows=L)
+                self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L)
+                self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"))
+                K.colsum(dK_img, Mi, CI, self.G(t2i + "k_proj.bias"))
+                K.colsum(dQ_img, Mi, CI, self.G(i2t + "q_proj.bias"))
+                K.colsum(dV_img, Mi, CI, self.G(t2i + "v_proj.bias"))
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
-                if ds4_leaf is not None:  # the out_proj leaf still reads ds4_b (= dkeys_in)
-                    torch.cuda.current_stream().wait_event(ds4_leaf)
                 self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)
-
-                def kqv_leaf(dKQV=dKQV, src=ls.kv_src_b):
-                    self._dw_pe(dKQV, src, RL, self._group(self.flat_grad, kq + [t2i + "v_proj.weight"], C),
-                                2 * CI, s.pe_b)
-                    K.colsum(dKQV, RL, 3 * CI, self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",
-                                                                            t2i + "v_proj.bias"], 0))
-                self._leaf(kqv_leaf, dKQV, ls.kv_src_b)
+                self._dw_pe(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq + [t2i + "v_proj.weight"], C),
+                            2 * CI, s.pe_b)
+                K.colsum(dKQV, RL, 3 * CI, self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",
+                                                                        t2i + "v_proj.bias"], 0))
                 dkeys = dkeys_in
             # LN1 / self attention
             dq, ds_b = self._ln_bwd(dq, ls.ln1)
@@ -781,7 +715,6 @@ class MaskDecoder(nn.Module):
         part = torch.empty(T * C, device=dev, dtype=f32)
         K.colsum(dtok, P, T * C, part)
         gtok.copy_(part[: gtok.numel()])
-        self._leaf_end()
         return G
 
     def _qin_bwd(self, dY_b, qin_b, wname, bname, R, dq, dtok):
