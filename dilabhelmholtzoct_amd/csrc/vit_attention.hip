@@ -367,6 +367,9 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   const int q = (blockIdx.x & 1) * (WNW * 32) + wave * 32 + l32;
   const bool qvalid = q < T;
   const int qc = qvalid ? q : T - 1;
+  // the second workgroup's last wave (query slots 224..255) has no real query: it skips the rel tables and
+  // every q.k / softmax / P.V, keeping only its share of the K/V loads and the barriers
+  const bool idle = __builtin_amdgcn_readfirstlane(q - l32) >= T;
   const int qh = qc / S, qw = qc % S;
   const float c1 = scale * L2E;
 
@@ -379,9 +382,11 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
 
   // rel_w for this lane half's 8 kw columns (units of the raw q.k: divided by the scale) and rel_h for the 14
   // key rows (log2 units), through this wave's scratch: table row j = q - i + 13
-  f32x16 init;
+  f32x16 init = (f32x16)0.0f;
   float relh[S];
-  {
+#pragma unroll
+  for (int i = 0; i < S; ++i) relh[i] = 0.0f;
+  if (!idle) {
     const f32x16 t = rel_block<HD, E>(Rw, 0, 2 * S - 1, qf, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
       init[r + 8] = v;
     }
   }
-  {
+  if (!idle) {
     const f32x16 t = rel_block<HD, E>(Rh, 0, 2 * S - 1, qf, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
@@ -416,9 +421,8 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
     raw_barrier();
     if (tile + 2 < NT)
       load_tile<HD, true, WNW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
+    if (idle) continue;  // all 32 query slots of this wave are padding: it only loads and syncs
     const char* slot = ring + (tile % NBUF) * G::TILE;
-    constexpr int dummy = 0;
-    (void)dummy;
     const int nb = tile == NT - 1 ? 1 : 2;  // 32-slot blocks holding keys (slots < 224)
     f32x16 sacc[2];
     float mh[4];  // raw max per half block (registers 0-7: key row kh0, 8-15: kh0 + 1)
