@@ -112,14 +112,16 @@ class GemmEventTimer:
                 out = orig(A, B, **kw)
                 e.record()
                 if lib.octsam_gemm_last_path() == 2:
-                    self.events.append((s, e))
-                    self.flops += 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
+                    fl = 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
                     # compulsory bytes: A, B read once, C written once (+ residual read), per launch
                     bt = kw.get("batch", 1)
                     osz = kw["out"].element_size()
                     r = kw.get("residual")
-                    self.bytes += bt * (2.0 * (kw["M"] + kw["N"]) * kw["K"] + kw["M"] * kw["N"] * osz +
-                                        (kw["M"] * kw["N"] * r.element_size() if r is not None else 0))
+                    by = bt * (2.0 * (kw["M"] + kw["N"]) * kw["K"] + kw["M"] * kw["N"] * osz +
+                               (kw["M"] * kw["N"] * r.element_size() if r is not None else 0))
+                    self.events.append((s, e, fl, by))
+                    self.flops += fl
+                    self.bytes += by
                 return out
             return orig(A, B, **kw)
 
@@ -136,9 +138,35 @@ class GemmEventTimer:
 
     def result(self):
         torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e in self.events)
+        ms = sum(s.elapsed_time(e) for s, e, _, _ in self.events)
         n = len(self.events)
         return ms, n, self.flops
+
+    def by_bound(self):
+        """The family's launches split by their compulsory arithmetic intensity against the MI355X ridge
+        (dense bf16 peak / HBM peak): compute-bound launches (encoder, neck) in TFLOP/s, memory-bound ones
+        (the decoder's K = 128-384 image-side projections) in GB/s of compulsory bytes."""
+        ridge = MI355X_BF16_DENSE_TFLOPS * 1e12 / (MI355X_HBM_GBS * 1e9)
+        out = {}
+        for name, sel in (("mfma_bound", lambda f, b: f / b >= ridge), ("hbm_bound", lambda f, b: f / b < ridge)):
+            ev = [(s.elapsed_time(e), f, b) for s, e, f, b in self.events if sel(f, b)]
+            if not ev:
+                continue
+            ms = sum(x[0] for x in ev)
+            fl = sum(x[1] for x in ev)
+            by = sum(x[2] for x in ev)
+            if name == "mfma_bound":
+                a = fl / (ms * 1e-3) / 1e12
+                out[name] = {"bound": "mfma", "achieved": round(a, 2), "peak": MI355X_BF16_DENSE_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(a / MI355X_BF16_DENSE_TFLOPS, 4), "launches": len(ev),
+                             "avg_launch_us": round(ms * 1e3 / len(ev), 2)}
+            else:
+                a = by / (ms * 1e-3) / 1e9
+                out[name] = {"bound": "hbm", "achieved": round(a, 1), "peak": MI355X_HBM_GBS, "unit": "GB/s",
+                             "frac": round(a / MI355X_HBM_GBS, 4), "launches": len(ev),
+                             "avg_launch_us": round(ms * 1e3 / len(ev), 2),
+                             "work": "compulsory bytes: A, B, C once (+ residual)"}
+        return out
 
 
 class CallTimer:
@@ -530,6 +558,7 @@ def main():
                     "compulsory_bytes_per_launch": round(timer.bytes / n),
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}
+            roof["family_by_intensity"] = timer.by_bound()
             roof.update(split)
 
     e2e = None
