@@ -134,17 +134,31 @@ struct Smem {
 };
 
 // bitonic sort of NP2 64-bit keys, ascending; every thread owns NP2/2/NTHR compare-exchange pairs per
-// stage and issues all their loads before any store (one LDS latency per stage, not one per pair)
+// stage and issues all their loads before any store (one LDS latency per stage, not one per pair).
+// Stages whose partner distance j is below a wave's chunk (NP2 / waves keys) stay inside that chunk, so
+// each wave runs them on its own chunk with only a wave-level ordering point; the workgroup barrier is
+// needed only around the stages with j >= chunk (6 of the 91 at NP2 = 8192).
 __device__ void sort_keys(uint64_t* keys, int tid) {
   constexpr int PP = NP2 / 2 / NTHR;
+  constexpr int NWAVE = NTHR / 64, CHUNK = NP2 / NWAVE;
+  const int lane = tid & 63, wave = tid >> 6;
+  bool wave_phase = false;  // the previous stage ran wave-locally (a workgroup barrier is owed)
   for (int k = 2; k <= NP2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
+      const bool local = j < CHUNK;
+      if (!local && wave_phase) __syncthreads();
       uint64_t a[PP], b[PP];
       int ia[PP];
 #pragma unroll
       for (int t = 0; t < PP; ++t) {
-        const int q = tid + t * NTHR;
-        const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+        int i;
+        if (local) {  // pair q of this wave's chunk
+          const int q = lane + t * 64;
+          i = wave * CHUNK + (((q & ~(j - 1)) << 1) | (q & (j - 1)));
+        } else {
+          const int q = tid + t * NTHR;
+          i = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+        }
         ia[t] = i;
         a[t] = keys[i];
         b[t] = keys[i | j];
@@ -157,9 +171,20 @@ __device__ void sort_keys(uint64_t* keys, int tid) {
         keys[ia[t]] = lo;
         keys[ia[t] | j] = hi;
       }
-      __syncthreads();
+      if (local) {
+        // the wave's own stores are visible to its next loads (LDS keeps a wave's accesses in order); keep
+        // the compiler from moving loads above them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_phase = true;
+      } else {
+        __syncthreads();
+        wave_phase = false;
+      }
     }
   }
+  if (wave_phase) __syncthreads();
 }
 
 // vertex id <-> bitmap position

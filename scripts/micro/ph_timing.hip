@@ -8,7 +8,7 @@
 #include "../../dilabhelmholtzoct_amd/csrc/cubical_ph.hip"
 namespace octsam { void set_error(const char* fmt, ...) { va_list a; va_start(a, fmt); vfprintf(stderr, fmt, a); va_end(a); } }
 int main() {
-  const int H = 50, W = 50, n = 16, mp = 1024;
+  const int H = 50, W = 50, n = 16, mp = 1250;
   std::mt19937 rng(0);
   std::normal_distribution<float> nd;
   for (int kind = 0; kind < 2; ++kind) {
