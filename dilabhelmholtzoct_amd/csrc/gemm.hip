@@ -1470,9 +1470,294 @@ int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// 256x192 variant of the 8-phase kernel for GEMMs whose 256-column tiles quantise badly on the chip (MLP2 /
+// proj at M = 32768, N = 768: 384 tiles = 1.5 waves of 256 CUs -> 512 tiles of 3/4 the work = 2 full waves).
+// Same phases, barriers and stagger; each wave owns 128 x 48 (3 column blocks of 16): Q(., 0) covers blocks
+// 0-1 (B-n0, 32 columns), Q(., 1) block 2 (B-n1, 16 columns). B-n1 is 64 rows per K-tile, one LDS-DMA op per
+// wave (A-lo, A-hi, B-n0 two each), so the counted waits are 9 / 7 / 8 in steady state (see launch notes).
+namespace ph8 {
+constexpr int BUF192 = 32768 + 192 * 128;  // A [256][64] + B [192][64] e16
+
+__device__ __forceinline__ void load_region192(const GemmK& p, const e16* A, const e16* B, int region, int row0,
+                                               int col0, int k0, char* buf, int wave, int lane) {
+  if (region < 2) {
+    load_region(p, A, B, region, row0, col0, k0, buf, wave, lane);
+    return;
+  }
+  const int nops = region == 2 ? 2 : 1;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u >= nops) break;
+    int rbase;
+    if (region == 2) {
+      const int j = wave * 2 + u;  // 16 groups of 8 rows: columns 0..31 of each wave column
+      rbase = (j >> 2) * 48 + (j & 3) * 8;
+    } else {
+      const int j = wave;  // 8 groups: columns 32..47 of each wave column
+      rbase = (j >> 1) * 48 + 32 + (j & 1) * 8;
+    }
+    const int r = rbase + (lane >> 3), slot = lane & 7;
+    const int c = slot ^ ((r >> 1) & 7);
+    int gr = col0 + r;
+    gr = gr < p.N ? gr : p.N - 1;
+    const e16* g = B + (long long)gr * p.ldb + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_ptr_t)(buf + 32768 + rbase * 128), 16, 0, 0);
+  }
+}
+
+// lean epilogue of a 128 x 48 wave tile: columns 0..31 (blocks 0, 1) as in epilogue_fast (permlane16_swap
+// to 8 consecutive columns per lane), columns 32..47 (block 2) straight from the transposed block: 4
+// consecutive columns per lane. FE as in epilogue_fast (kinds 1: e16 C, 4: fp32 C + in-place fp32 residual).
+template <int ACT, int FE, int MI0, int NMI>
+__device__ __forceinline__ void epilogue_n192(const GemmK& p, f32x4 (&acc)[8][3], int bz, int row0, int col0,
+                                              int lane) {
+  constexpr bool CF32 = FE == 4, RES = FE == 4;
+  static_assert(FE == 1 || FE == 4, "n192 epilogue kinds: 1 (e16 C), 4 (fp32 C + fp32 residual)");
+  constexpr int ES = CF32 ? 4 : 2;
+  const int q = lane >> 4;
+  const int cofs = 16 * (q & 1) + 8 * (q >> 1);
+  const int rows_left = max(0, p.M - row0);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((char*)p.C + (bz * p.sC + (long long)row0 * p.ldc + col0) * ES), (short)0,
+      rows_left * (int)p.ldc * ES, 0x00020000);
+  __amdgpu_buffer_rsrc_t rr = rc;
+  if constexpr (RES)
+    rr = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.R + (bz * p.sR + (long long)row0 * p.ldr + col0) * ES),
+                                           (short)0, rows_left * (int)p.ldr * ES, 0x00020000);
+  // bias: 8 columns (pair part) + 4 columns (block 2) per lane
+  float bp[8], bt[4];
+  if (p.bias) {
+    const f32x4 x0 = *(const f32x4*)(p.bias + col0 + cofs), x1 = *(const f32x4*)(p.bias + col0 + cofs + 4);
+    const f32x4 x2 = *(const f32x4*)(p.bias + col0 + 32 + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bp[e] = x0[e];
+      bp[4 + e] = x1[e];
+      bt[e] = x2[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bp[e] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bt[e] = 0.0f;
+  }
+#pragma unroll
+  for (int jj = 0; jj < NMI; ++jj) {
+    const int j = MI0 + jj;
+    const uint32_t rowoff = (uint32_t)((16 * j + (lane & 15)) * (int)p.ldc * ES);
+    const uint32_t rowoff_r = (uint32_t)((16 * j + (lane & 15)) * (int)p.ldr * ES);
+    // blocks 0, 1 -> 8 consecutive columns
+    float v[8];
+    {
+      const u32x4 x = __builtin_bit_cast(u32x4, acc[j][0]);
+      const u32x4 y = __builtin_bit_cast(u32x4, acc[j][1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t xi = x[i], yi = y[i];
+        const auto r = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
+        v[i] = __builtin_bit_cast(float, (uint32_t)r[0]);
+        v[4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
+      }
+    }
+    float w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = acc[j][2][i];
+    const uint32_t op = rowoff + (uint32_t)(cofs * ES), ot = rowoff + (uint32_t)((32 + 4 * q) * ES);
+    const uint32_t opr = rowoff_r + (uint32_t)(cofs * ES), otr = rowoff_r + (uint32_t)((32 + 4 * q) * ES);
+    float rp[8], rt[4];
+    if constexpr (RES) {
+      const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, opr, 0, 0));
+      const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, opr + 16, 0, 0));
+      const f32x4 c = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, otr, 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rp[e] = a[e];
+        rp[4 + e] = b[e];
+        rt[e] = c[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = act_apply<ACT>(v[e] * p.alpha + bp[e]);
+      if constexpr (RES) v[e] += rp[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      w[e] = act_apply<ACT>(w[e] * p.alpha + bt[e]);
+      if constexpr (RES) w[e] += rt[e];
+    }
+    if constexpr (CF32) {
+      const f32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]}, c = {w[0], w[1], w[2], w[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rc, op, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rc, op + 16, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c), rc, ot, 0, 0);
+    } else {
+      e16x8 h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = (e16)v[e];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), rc, op, 0, 0);
+      e16x4 t4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t4[e] = (e16)w[e];
+      typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, t4), rc, ot, 0, 0);
+    }
+  }
+}
+}  // namespace ph8
+
+#define PH8_MFMA_N192(MH, NH, BF, NNI, FIRST)                                                            \
+  __builtin_amdgcn_s_setprio(1);                                                                          \
+  _Pragma("unroll") for (int kb = 0; kb < 2; ++kb)                                                       \
+  _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                                       \
+  _Pragma("unroll") for (int ni = 0; ni < NNI; ++ni)                                                     \
+    acc[(MH) * 4 + mi][(NH) * 2 + ni] = mma16(BF[ni][kb], af[mi][kb],                                     \
+        (FIRST && kb == 0) ? (f32x4)0.0f : acc[(MH) * 4 + mi][(NH) * 2 + ni], 0, 0, 0);                   \
+  __builtin_amdgcn_s_setprio(0);
+
+template <int EPI, int FE>
+__global__ __launch_bounds__(512, 2) void gemm8n192_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = bid / per_batch, rem = bid - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 192;
+  const e16* A = (const e16*)p.A + bz * p.sA;
+  const e16* B = (const e16*)p.B + bz * p.sB;
+  const int nk = p.K / 64;
+
+  f32x4 acc[8][3];  // written by the first K-step's zero-accumulator MFMAs (K >= 64 host-checked)
+  e16x8 af[4][2], b0[2][2], b1[1][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 48 + (lane & 15), kq = lane >> 4;
+
+  // prologue: K-tile 0 (A-lo, B-n0 | B-n1 | A-hi), K-tile 1 (A-lo, B-n0 | B-n1); ops per wave 2,2,1,2 | 2,2,1
+  ph8::load_region192(p, A, B, 0, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region192(p, A, B, 2, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region192(p, A, B, 3, row0, col0, 0, gsm, wave, lane);
+  ph8::load_region192(p, A, B, 1, row0, col0, 0, gsm, wave, lane);
+  if (nk > 1) {
+    ph8::load_region192(p, A, B, 0, row0, col0, 64, gsm + ph8::BUF192, wave, lane);
+    ph8::load_region192(p, A, B, 2, row0, col0, 64, gsm + ph8::BUF192, wave, lane);
+    ph8::load_region192(p, A, B, 3, row0, col0, 64, gsm + ph8::BUF192, wave, lane);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A-lo, B-n0 of K-tile 0 landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    char* cur = gsm + (t & 1) * ph8::BUF192;
+    char* nxt = gsm + ((t + 1) & 1) * ph8::BUF192;
+    const char* ca = cur;
+    const char* cb = cur + 32768;
+    const bool h1 = t + 1 < nk, h2 = t + 2 < nk;
+    const bool first = t == 0;
+    // ---- phase 0: Q(0,0) — A-lo, B-n0
+    if (h1) ph8::load_region192(p, A, B, 1, row0, col0, (t + 1) * 64, nxt, wave, lane);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + mi * 16, kb * 4 + kq);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b0[ni][kb] = ph8::frag(cb, brow + ni * 16, kb * 4 + kq);
+    }
+    if (h1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // retire B-n1(t)
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (first) { PH8_MFMA_N192(0, 0, b0, 2, true) } else { PH8_MFMA_N192(0, 0, b0, 2, false) }
+    raw_barrier();
+    // ---- phase 1: Q(0,1) — B-n1
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) b1[0][kb] = ph8::frag(cb, brow + 32, kb * 4 + kq);
+    if (h1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // retire A-hi(t)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (first) { PH8_MFMA_N192(0, 1, b1, 1, true) } else { PH8_MFMA_N192(0, 1, b1, 1, false) }
+    raw_barrier();
+    // ---- phase 2: Q(1,0) — A-hi; restage A-lo, B-n0 of K-tile t+2
+    if (h2) {
+      ph8::load_region192(p, A, B, 0, row0, col0, (t + 2) * 64, cur, wave, lane);
+      ph8::load_region192(p, A, B, 2, row0, col0, (t + 2) * 64, cur, wave, lane);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][kb] = ph8::frag(ca, arow + 64 + mi * 16, kb * 4 + kq);
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (first) { PH8_MFMA_N192(1, 0, b0, 2, true) } else { PH8_MFMA_N192(1, 0, b0, 2, false) }
+    raw_barrier();
+    // ---- phase 3: Q(1,1); restage B-n1 of K-tile t+2; retire A-lo, B-n0 of K-tile t+1
+    if (h2) ph8::load_region192(p, A, B, 3, row0, col0, (t + 2) * 64, cur, wave, lane);
+    if (h2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (h1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    raw_barrier();
+    if (first) { PH8_MFMA_N192(1, 1, b1, 1, true) } else { PH8_MFMA_N192(1, 1, b1, 1, false) }
+    raw_barrier();
+  }
+  if (wr == 0) raw_barrier();  // balance the stagger
+  if constexpr (FE == 1) {
+    ph8::epilogue_n192<EPI, FE, 0, 8>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+  } else {
+    ph8::epilogue_n192<EPI, FE, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+    ph8::epilogue_n192<EPI, FE, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+  }
+}
+
+template <int EPI, int FE>
+int launch_gemm8n192(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = a->N / 192;
+  constexpr int LDS = 2 * ph8::BUF192;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8n192_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
+  hipLaunchKernelGGL((gemm8n192_kernel<EPI, FE>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+// 256x192 tiles when they fill the chip's waves better than 256x256 ones (3/4 of the work per tile);
+// g_n192 = 0 (fast path 21, A/B diagnostics) keeps the 256x256 kernels
+static int g_n192 = 1;
+inline bool prefer_n192(const octsam_gemm_args* a, int n_cu) {
+  if (a->N % 192 != 0 || a->K < 64) return false;
+  const long long tm = (a->M + 255) / 256;
+  const long long t256 = tm * ((a->N + 255) / 256) * a->batch, t192 = tm * (a->N / 192) * a->batch;
+  const double w256 = (double)((t256 + n_cu - 1) / n_cu), w192 = 0.75 * (double)((t192 + n_cu - 1) / n_cu);
+  return w192 < w256 - 0.2;
+}
+
 template <int DBG, int EPI>
 int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   if constexpr (EPI >= 0 && DBG == 0) {
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (n_cu <= 0) n_cu = 256;
+    }
+    if (g_n192 && (k.fast_epi == 1 || k.fast_epi == 4) && a->row_map == nullptr &&
+        (a->R == nullptr || a->r_blk == 0) && prefer_n192(a, n_cu)) {
+      if (k.fast_epi == 1) return launch_gemm8n192<EPI, 1>(k, a, s);
+      return launch_gemm8n192<EPI, 4>(k, a, s);
+    }
     switch (k.fast_epi) {  // the kinds the encoder and decoder use
       case 1: return launch_gemm8_fe<DBG, EPI, 1>(k, a, s);    // e16 C
       case 2: return launch_gemm8_fe<DBG, EPI, 2>(k, a, s);    // fp32 C
@@ -1797,6 +2082,7 @@ int& last_path() { static thread_local int v = 0; return v; }
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_small = (enable & 256) ? 0 : 1;
   g_use_glds = enable & 255;
+  g_n192 = g_use_glds == 21 ? 0 : 1;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
 #endif

@@ -53,7 +53,7 @@ for name, M, N, Kd, act, res in SHAPES:
     ob = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     row = {"name": name, "M": M, "N": N, "K": Kd}
     variants = [("default", 1), ("single", 11), ("relax", 13), ("p1tile", 14), ("p_nostore", 16), ("p_tile0", 17),
-                ("general", 18), ("nopersist", 20), ("noepi", 6), ("noloop", 7), ("blaslt", None)]
+                ("general", 18), ("nopersist", 20), ("no192", 21), ("noepi", 6), ("noloop", 7), ("blaslt", None)]
     best = {}
     for rnd in range(3):  # round-robin, min over rounds: no variant always runs first after a clock ramp
         for tag, fast in variants:

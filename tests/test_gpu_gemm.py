@@ -292,6 +292,36 @@ def test_gemm8_lean_epilogue_kinds(cuda, kind, act, N):
     assert _rel(outs[0].float(), outs[1].float()) < 1e-6 if cdt == torch.float32 else torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K,kind", [(32768, 768, 3072, "f32_res"), (32768, 768, 768, "f32_res"),
+                                         (1100, 768, 192, "f32_res"), (1100, 768, 128, "e16"),
+                                         (32768, 2304, 768, "e16")])
+@pytest.mark.parametrize("act", [0, 2])
+def test_gemm8_n192_tiles(cuda, M, N, K, kind, act):
+    """256x192 tiles (chosen when they fill the chip's waves better: MLP2 / proj at M = 32768): against torch fp32
+    and bit-identical to the 256x256 kernel (fast path 21 keeps those), ragged M, in-place fp32 residual."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + act)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    f32 = kind == "f32_res"
+    X0 = torch.randn(M, N, generator=g).to(cuda, torch.float32 if f32 else torch.bfloat16)
+    outs = []
+    for fast in (11, 21 | 0):  # 11: no persistent kernel (n192 eligible); 21: 256x256 tiles only
+        lib.octsam_gemm_set_fast_path(fast | 256)
+        out = X0.clone()
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, act=act, residual=out if f32 else None)
+        assert lib.octsam_gemm_last_path() == 2
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    pre = A.float() @ W.float().t() + bias
+    ref = (F.gelu(pre) if act == 2 else pre) + (X0.float() if f32 else 0.0)
+    for out in outs:
+        assert _rel(out.float(), ref) < (1e-5 if f32 else 8e-3)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("a_mode,b_mode", [(1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("shape", [(1104, 392, 192, 2), (256, 256, 128, 64), (128, 264, 64, 40)])
 def test_gemm_fast_path_kmajor(cuda, a_mode, b_mode, shape):
