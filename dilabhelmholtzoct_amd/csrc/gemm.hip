@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(GemmK p, int batch, int 
     if (++cc.kt == nk) {  // last K-step of tile cc.i: epilogue while steps g+1, g+2 load
       const int ebz = (dbg & 8) ? 0 : (first + cc.i * stride) / per_batch;
       const int er0 = ((dbg & 8) ? 0 : cc.row0) + wr * 128, ec0 = ((dbg & 8) ? 0 : cc.col0) + wc * 64;
-      if constexpr (FE == 3 || FE == 11) {  // residual kinds: quarters (the loaded residual must fit too)
+      if constexpr (FE == 11) {  // residual kind: quarters (the loaded residual must fit too)
         ph8::epilogue_fast<EPI, FE, true, 0, 2>(pe, acc, ebz, er0, ec0, lane, lbias);
         ph8::epilogue_fast<EPI, FE, true, 2, 2>(pe, acc, ebz, er0, ec0, lane, lbias);
         ph8::epilogue_fast<EPI, FE, true, 4, 2>(pe, acc, ebz, er0, ec0, lane, lbias);
@@ -1984,7 +1984,6 @@ template <int EPI>
 int launch_gemm8p(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, int dbg) {
   if (k.fast_epi == 1) return launch_gemm8p_fe<EPI, 1>(k, a, s, dbg);
   if constexpr (EPI == 0) {  // decoder image-side projections: e16 C + e16 (broadcast) residual, K <= 512
-    if (k.fast_epi == 3) return launch_gemm8p_fe<EPI, 3>(k, a, s, dbg);
     if (k.fast_epi == 11) return launch_gemm8p_fe<EPI, 11>(k, a, s, dbg);
   }
   // (fp32 output + GELU would spill in this kernel: general epilogue)
@@ -2189,7 +2188,7 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // (an e16 residual is allowed at small K: its loads drain the next tile's prefetch, which is the whole
       // next tile there anyway, and the tile's load latency still overlaps the epilogue)
       const bool res_small_k =
-          a->R != nullptr && (k.fast_epi == 3 || k.fast_epi == 11) && a->K <= 512 && a->act == 0;
+          a->R != nullptr && k.fast_epi == 11 && a->K <= 512 && a->act == 0;  // (kind 3 measured slower)
       const bool persist = (a->R == nullptr || res_small_k) && a->row_map == nullptr && a->N <= ph8::BIAS_MAX &&
                            g_use_glds != 11 && g_use_glds != 20 &&
                            (long long)a->M * a->lda * 2 < (1LL << 31) && (long long)a->N * a->ldb * 2 < (1LL << 31);
