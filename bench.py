@@ -204,11 +204,12 @@ class CallTimer:
         return sum(s.elapsed_time(e) for s, e in self.events), len(self.events), self.total
 
 
-def attn_flops(qkv, out, rh, rw, *, nseq, side, heads, head_dim=64):
+def attn_flops(qkv, out, rh, rw, *, nseq, side, heads, grid=0, pad_row=None):
     """QK^T and PV of one octsam_vit_attention launch: 4 * T^2 * head_dim * heads * nseq, T = side^2 (the
-    windowed layers' padded 14x14 windows included, as the reference computes them)."""
+    windowed layers' padded 14x14 windows included, as the reference computes them); head_dim from the
+    rel-pos tables (64 vit-b/l, 80 vit-h)."""
     T = side * side
-    return 4.0 * T * T * head_dim * heads * nseq
+    return 4.0 * T * T * rh.shape[-1] * heads * nseq
 
 
 def make_batch(args, rank, device, processor):

@@ -119,11 +119,9 @@ __device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0,
   return acc;
 }
 
-// Key slots key0 .. key0+63 -> ring slot by NWV waves, every wave the same number of ops: per 8-row group
-// 1 KiB (8 rows x 128 B) of each first-64-dim image, and for head dim 80 256 B (8 rows x 32 B) of each tail. Global layers: slot = key.
-// Windowed layers (WIN): slot = 16 kh + kw (key rows padded 14 -> 16 columns, 14 rows -> 16), padding slots
-// load the window's last key (their scores are masked).
-template <int HD, bool WIN, int NWV, typename E>
+// Global layers: keys key0 .. key0+63 -> ring slot by NWV waves, every wave the same number of ops: per 8-row
+// group 1 KiB (8 rows x 128 B) of each first-64-dim image, and for head dim 80 256 B (8 rows x 32 B) of each tail.
+template <int HD, int NWV, typename E>
 __device__ __forceinline__ void load_tile(const E* kbase, const E* vbase, int ld, int key0, char* slot, int wave,
                                           int lane) {
   using G = Geo<HD>;
@@ -131,9 +129,7 @@ __device__ __forceinline__ void load_tile(const E* kbase, const E* vbase, int ld
   for (int i = 0; i < 8 / NWV; ++i) {  // 8-row groups of this wave
     const int grp = wave + NWV * i;
     const int r = grp * 8 + (lane >> 3), sl = lane & 7;
-    int key = key0 + r;
-    if constexpr (WIN) key = min((key >> 4) * 14 + min(key & 15, 13), 195);
-    const long long row = (long long)key * ld;
+    const long long row = (long long)(key0 + r) * ld;
     const int ck = sl ^ ((r >> 1) & 7), cv = sl ^ (((r >> 1) & 1) << 2);
     __builtin_amdgcn_global_load_lds((const void*)(kbase + row + ck * 8), (lds_ptr_t)(slot + G::K_OFF + grp * 1024),
                                      16, 0, 0);
@@ -143,6 +139,70 @@ __device__ __forceinline__ void load_tile(const E* kbase, const E* vbase, int ld
       __builtin_amdgcn_global_load_lds((const void*)(kbase + row + 64 + 2 * sl),
                                        (lds_ptr_t)(slot + G::KT_OFF + grp * 256), 4, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(vbase + row + 64 + 2 * sl),
+                                       (lds_ptr_t)(slot + G::VT_OFF + grp * 256), 4, 0, 0);
+    }
+  }
+}
+
+// Rows of one window's 196 tokens. Window-ordered input (grid == 0): row t of the window's block of the qkv
+// tensor (window_partition already applied, padding rows present). Token-ordered input (grid > 0, the image's
+// grid x grid tokens row-major, B images): the window's token (ty, tx) is image row (y0 + ty, x0 + tx); tokens
+// past the grid (window_partition's zero padding, whose qkv row is the bias row) read `pad`, and their
+// outputs are dropped (window_unpartition), so the padded rows are never formed.
+template <typename E> struct WinRows {
+  const E* base;
+  const E* pad;
+  long long img;  // first row of the window's image (token-ordered)
+  int ld, grid, y0, x0;
+  __device__ __forceinline__ WinRows(const E* qkv, const E* pad_, int win, int ld_, int grid_) : pad(pad_), ld(ld_), grid(grid_) {
+    if (grid == 0) {
+      base = qkv + (long long)win * 196 * ld;
+      img = 0; y0 = 0; x0 = 0;
+    } else {
+      const int nw = (grid + 13) / 14, b = win / (nw * nw), r = win - b * nw * nw, wy = r / nw;
+      base = qkv;
+      img = (long long)b * grid * grid;
+      y0 = 14 * wy;
+      x0 = 14 * (r - wy * nw);
+    }
+  }
+  __device__ __forceinline__ bool real(int t) const {
+    const int ty = t / 14;
+    return grid == 0 || (y0 + ty < grid && x0 + t - 14 * ty < grid);
+  }
+  __device__ __forceinline__ long long row(int t) const {  // token-ordered row (grid > 0) or window row
+    if (grid == 0) return t;
+    const int ty = t / 14;
+    return img + (long long)(y0 + ty) * grid + (x0 + t - 14 * ty);
+  }
+  __device__ __forceinline__ const E* at(int t) const {
+    if (grid == 0) return base + (long long)t * ld;
+    return real(t) ? base + row(t) * ld : pad;
+  }
+};
+
+// Windowed layers: key slots key0 .. key0+63 (slot = 16 kh + kw; key rows padded 14 -> 16 columns, 14 rows ->
+// 16, padding slots load the window's last key, their scores are masked) -> ring slot; same per-wave ops as
+// load_tile. koff / voff: the head's K / V columns within a qkv row.
+template <int HD, int NWV, typename E>
+__device__ __forceinline__ void load_tile_win(const WinRows<E>& wr, int koff, int voff, int key0, char* slot,
+                                              int wave, int lane) {
+  using G = Geo<HD>;
+#pragma unroll
+  for (int i = 0; i < 8 / NWV; ++i) {
+    const int grp = wave + NWV * i;
+    const int r = grp * 8 + (lane >> 3), sl = lane & 7;
+    const int key = key0 + r;
+    const E* rp = wr.at(min((key >> 4) * 14 + min(key & 15, 13), 195));
+    const int ck = sl ^ ((r >> 1) & 7), cv = sl ^ (((r >> 1) & 1) << 2);
+    __builtin_amdgcn_global_load_lds((const void*)(rp + koff + ck * 8), (lds_ptr_t)(slot + G::K_OFF + grp * 1024),
+                                     16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(rp + voff + cv * 8), (lds_ptr_t)(slot + G::V_OFF + grp * 1024),
+                                     16, 0, 0);
+    if constexpr (G::TAIL) {
+      __builtin_amdgcn_global_load_lds((const void*)(rp + koff + 64 + 2 * sl),
+                                       (lds_ptr_t)(slot + G::KT_OFF + grp * 256), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(rp + voff + 64 + 2 * sl),
                                        (lds_ptr_t)(slot + G::VT_OFF + grp * 256), 4, 0, 0);
     }
   }
@@ -277,8 +337,8 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
 
   const E* kbase = base + D + head * HD;
   const E* vbase = base + 2 * D + head * HD;
-  load_tile<HD, false, NW, E>(kbase, vbase, ld, 0, ring, wave, lane);
-  load_tile<HD, false, NW, E>(kbase, vbase, ld, 64, ring + G::TILE, wave, lane);
+  load_tile<HD, NW, E>(kbase, vbase, ld, 0, ring, wave, lane);
+  load_tile<HD, NW, E>(kbase, vbase, ld, 64, ring + G::TILE, wave, lane);
 
   f32x16 acc_o[G::NTD];
 #pragma unroll
@@ -290,7 +350,7 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
     else wait_vm<0>();
     raw_barrier();
     if (tile + 2 < NT)
-      load_tile<HD, false, NW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
+      load_tile<HD, NW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
     const char* slot = ring + (tile % NBUF) * G::TILE;
     f32x16 sacc[2];
 #pragma unroll
@@ -351,7 +411,8 @@ static_assert(w_smem<64>() <= 160 * 1024 / 3, "three windowed workgroups per CU 
 template <int HD, typename E>
 __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __restrict__ qkv, E* __restrict__ out,
                                                               const float* __restrict__ Rh,
-                                                              const float* __restrict__ Rw, int heads, float scale) {
+                                                              const float* __restrict__ Rw, int heads, float scale,
+                                                              int grid, const E* __restrict__ pad) {
   using G = Geo<HD>;
   using V8 = typename ET<E>::v8;
   constexpr int S = 14, T = 196, NT = 4;  // 224 key slots in 4 tiles (the last one half used)
@@ -363,10 +424,10 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   // block x = (head, query half) fastest: the 2*heads workgroups of a window read the same qkv rows together
   const int head = blockIdx.x >> 1, win = blockIdx.y;
   const int D = heads * HD, ld = 3 * D;
-  const E* base = qkv + (long long)win * T * ld;
+  const WinRows<E> wr(qkv, pad, win, ld, grid);
   const int q = (blockIdx.x & 1) * (WNW * 32) + wave * 32 + l32;
-  const bool qvalid = q < T;
-  const int qc = qvalid ? q : T - 1;
+  const int qc = q < T ? q : T - 1;
+  const bool qvalid = q < T && wr.real(q);
   // the second workgroup's last wave (query slots 224..255) has no real query: it skips the rel tables and
   // every q.k / softmax / P.V, keeping only its share of the K/V loads and the barriers
   const bool idle = __builtin_amdgcn_readfirstlane(q - l32) >= T;
@@ -374,11 +435,10 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   const float c1 = scale * L2E;
 
   V8 qf[G::NKS];
-  load_q<HD, E>(base + (long long)qc * ld + head * HD, qf, h);
-  const E* kbase = base + D + head * HD;
-  const E* vbase = base + 2 * D + head * HD;
-  load_tile<HD, true, WNW, E>(kbase, vbase, ld, 0, ring, wave, lane);
-  load_tile<HD, true, WNW, E>(kbase, vbase, ld, 64, ring + G::TILE, wave, lane);
+  load_q<HD, E>(wr.at(qc) + head * HD, qf, h);
+  const int koff = D + head * HD, voff = 2 * D + head * HD;
+  load_tile_win<HD, WNW, E>(wr, koff, voff, 0, ring, wave, lane);
+  load_tile_win<HD, WNW, E>(wr, koff, voff, 64, ring + G::TILE, wave, lane);
 
   // rel_w for this lane half's 8 kw columns (units of the raw q.k: divided by the scale) and rel_h for the 14
   // key rows (log2 units), through this wave's scratch: table row j = q - i + 13
@@ -420,7 +480,7 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
     else wait_vm<0>();
     raw_barrier();
     if (tile + 2 < NT)
-      load_tile<HD, true, WNW, E>(kbase, vbase, ld, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
+      load_tile_win<HD, WNW, E>(wr, koff, voff, (tile + 2) * 64, ring + ((tile + 2) % NBUF) * G::TILE, wave, lane);
     if (idle) continue;  // all 32 query slots of this wave are padding: it only loads and syncs
     const char* slot = ring + (tile % NBUF) * G::TILE;
     const int nb = tile == NT - 1 ? 1 : 2;  // 32-slot blocks holding keys (slots < 224)
@@ -471,12 +531,13 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   }
   if (!qvalid) return;
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  store_out<HD, E>(out + ((long long)win * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
+  const long long orow = grid == 0 ? (long long)win * T + q : wr.row(q);
+  store_out<HD, E>(out + orow * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
 template <int HD, typename E>
-int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nseq, int side, int heads,
-           hipStream_t s) {
+int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nseq, int side, int heads, int grid,
+           const void* pad, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HD);
   if (side == 64) {
     static bool attr = false;
@@ -495,7 +556,7 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
       attr = true;
     }
     hipLaunchKernelGGL((vit_attn_window_kernel<HD, E>), dim3(2 * heads, nseq, 1), dim3(WTHR), w_smem<HD>(), s,
-                       (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+                       (const E*)qkv, (E*)out, Rh, Rw, heads, scale, grid, (const E*)pad);
   }
   return 0;
 }
@@ -504,7 +565,7 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
 
 extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w,
                                     int32_t nseq, int32_t side, int32_t heads, int32_t head_dim, int32_t fp16,
-                                    void* stream) {
+                                    int32_t grid, const void* pad_row, void* stream) {
   OCTSAM_CHECK_ARG(qkv && out && rel_pos_h && rel_pos_w && nseq > 0 && heads > 0 && nseq <= 65535,
                    "octsam_vit_attention: bad args");
   OCTSAM_CHECK_ARG(head_dim == 64 || head_dim == 80, "octsam_vit_attention: head_dim must be 64 or 80 (got %d)",
@@ -514,13 +575,17 @@ extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel
   OCTSAM_CHECK_ARG(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)rel_pos_h & 15) == 0 &&
                        ((uintptr_t)rel_pos_w & 15) == 0,
                    "octsam_vit_attention: operands must be 16-B aligned");
+  OCTSAM_CHECK_ARG(grid == 0 || (side == 14 && grid > 0 && grid <= 4096 && pad_row && ((uintptr_t)pad_row & 15) == 0 &&
+                                  nseq % (((grid + 13) / 14) * ((grid + 13) / 14)) == 0),
+                   "octsam_vit_attention: token-ordered windows need side 14, nseq = images * windows and an aligned "
+                   "pad row");
   hipStream_t s = (hipStream_t)stream;
   if (head_dim == 64)
-    fp16 ? launch<64, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s)
-         : launch<64, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s);
+    fp16 ? launch<64, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, grid, pad_row, s)
+         : launch<64, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, grid, pad_row, s);
   else
-    fp16 ? launch<80, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s)
-         : launch<80, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, s);
+    fp16 ? launch<80, f16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, grid, pad_row, s)
+         : launch<80, bf16>(qkv, out, rel_pos_h, rel_pos_w, nseq, side, heads, grid, pad_row, s);
   OCTSAM_LAUNCH_CHECK("octsam_vit_attention");
   return 0;
 }

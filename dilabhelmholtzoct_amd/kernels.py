@@ -140,19 +140,30 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
 
 
 def vit_attention(qkv: torch.Tensor, out: torch.Tensor, rel_pos_h: torch.Tensor, rel_pos_w: torch.Tensor, *,
-                  nseq: int, side: int, heads: int) -> torch.Tensor:
+                  nseq: int, side: int, heads: int, grid: int = 0,
+                  pad_row: torch.Tensor | None = None) -> torch.Tensor:
     """Fused SAM ViT attention with decomposed rel-pos bias; see octsam_vit_attention. head_dim from the
-    rel-pos tables (64 or 80), element type from qkv (bf16 or fp16)."""
-    _require_cuda(qkv, out, rel_pos_h, rel_pos_w)
+    rel-pos tables (64 or 80), element type from qkv (bf16 or fp16). grid > 0 (windowed layers): qkv / out are
+    token-ordered over images of grid x grid tokens and pad_row ([3 * heads * head_dim], the qkv bias in qkv's
+    type) stands for window_partition's padding tokens."""
+    _require_cuda(qkv, out, rel_pos_h, rel_pos_w, pad_row)
     if qkv.dtype not in (torch.bfloat16, torch.float16) or out.dtype != qkv.dtype:
         raise ValueError("vit_attention expects bf16 or fp16 qkv / out of the same type")
     hd = rel_pos_h.shape[-1]
-    if qkv.numel() != nseq * side * side * 3 * heads * hd or out.numel() != nseq * side * side * heads * hd:
+    tokens = nseq * side * side
+    if grid:
+        nw = (grid + side - 1) // side
+        if side != 14 or nseq % (nw * nw):
+            raise ValueError("token-ordered windows need side 14 and nseq = images * windows per image")
+        if pad_row is None or pad_row.dtype != qkv.dtype or pad_row.numel() != 3 * heads * hd:
+            raise ValueError("token-ordered windows need pad_row [3 * heads * head_dim] of qkv's type")
+        tokens = nseq // (nw * nw) * grid * grid
+    if qkv.numel() != tokens * 3 * heads * hd or out.numel() != tokens * heads * hd:
         raise ValueError("qkv / out shape does not match nseq / side / heads / head_dim")
     rh = rel_pos_h.float().contiguous()  # (named, so a converted copy outlives the launch)
     rw = rel_pos_w.float().contiguous()
     _lib.call("octsam_vit_attention", ptr(qkv), ptr(out), ptr(rh), ptr(rw), nseq, side, heads, hd,
-              int(qkv.dtype == torch.float16))
+              int(qkv.dtype == torch.float16), grid, ptr(pad_row))
     return out
 
 

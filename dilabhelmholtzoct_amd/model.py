@@ -91,7 +91,6 @@ class VisionEncoder(nn.Module):
             for i in range(cfg.num_hidden_layers)])
         self.neck = VisionNeck(cfg)
         self._wcache: dict = {}
-        self._maps: dict = {}
         # 16-bit operand type of the encoder's MFMA work: bf16 (BASELINE configs[1..3]) or fp16 (configs[4]);
         # the residual stream, LayerNorm statistics and accumulation stay fp32
         self.compute_dtype = torch.bfloat16
@@ -116,25 +115,6 @@ class VisionEncoder(nn.Module):
             ent = (tag, t.float().contiguous())
             self._wcache[key] = ent
         return ent[1]
-
-    def _window_map(self, B: int, device) -> torch.Tensor:
-        """windowed row -> image row (b*4096 + y*64 + x) or -1 for padding (window_partition,
-        hf:modeling_sam.py:900-952)."""
-        key = (B, str(device))
-        if key not in self._maps:
-            ws, g = self.config.window_size, self.config.image_size // self.config.patch_size
-            nw = (g + ws - 1) // ws
-            b = torch.arange(B).view(B, 1, 1, 1, 1)
-            wy = torch.arange(nw).view(1, nw, 1, 1, 1)
-            wx = torch.arange(nw).view(1, 1, nw, 1, 1)
-            ty = torch.arange(ws).view(1, 1, 1, ws, 1)
-            tx = torch.arange(ws).view(1, 1, 1, 1, ws)
-            y = wy * ws + ty
-            x = wx * ws + tx
-            idx = b * g * g + y * g + x
-            idx = torch.where((y < g) & (x < g), idx, torch.full_like(idx, -1))
-            self._maps[key] = idx.reshape(-1).to(torch.int32).to(device)
-        return self._maps[key]
 
     @torch.no_grad()
     def forward_nhwc(self, pixel_values: torch.Tensor) -> torch.Tensor:
@@ -164,38 +144,29 @@ class VisionEncoder(nn.Module):
                r_remap=(L, B))
         xn = torch.empty(M, D, device=dev, dtype=e16)
         mlp_h = torch.empty(M, cfg.mlp_dim, device=dev, dtype=e16)
-        wmap = None
         for li, layer in enumerate(self.layers):
             at = layer.attn
             ws = layer.window_size
             pre = f"l{li}."
             ln1w, ln1b = self._wf(pre + "ln1w", layer.layer_norm1.weight), self._wf(pre + "ln1b", layer.layer_norm1.bias)
+            # windowed layers stay token-ordered: window_partition / window_unpartition (hf:modeling_sam.py:
+            # 900-952, 960-966) happen inside the attention kernel's row addressing; the padding tokens' qkv
+            # (Linear of a zero row = the bias) is one row, not 6432 computed ones
+            K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xn)
+            qkv = torch.empty(M, 3 * D, device=dev, dtype=e16)
+            K.gemm(xn, self._w(pre + "qkv", at.qkv.weight), M=M, N=3 * D, K=D, out=qkv,
+                   bias=self._wf(pre + "qkvb", at.qkv.bias))
+            ao = torch.empty(M, D, device=dev, dtype=e16)
+            rh, rw = self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w)
             if ws > 0:
-                if wmap is None:
-                    wmap = self._window_map(B, dev)
-                Mw = wmap.numel()
-                xw = torch.empty(Mw, D, device=dev, dtype=e16)
-                K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xw, src_rows=wmap)
-                qkv = torch.empty(Mw, 3 * D, device=dev, dtype=e16)
-                K.gemm(xw, self._w(pre + "qkv", at.qkv.weight), M=Mw, N=3 * D, K=D, out=qkv,
-                       bias=self._wf(pre + "qkvb", at.qkv.bias))
-                ao = torch.empty(Mw, D, device=dev, dtype=e16)
-                K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
-                                nseq=Mw // (ws * ws), side=ws, heads=heads)
-                K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=Mw, N=D, K=D, out=x,
-                       bias=self._wf(pre + "projb", at.proj.bias), residual=x, row_map=wmap)
-                del xw, qkv, ao
+                nw = (g + ws - 1) // ws
+                K.vit_attention(qkv, ao, rh, rw, nseq=B * nw * nw, side=ws, heads=heads, grid=g,
+                                pad_row=self._w(pre + "qkvpad", at.qkv.bias))
             else:
-                K.layernorm_fwd(x, ln1w, ln1b, cfg.layer_norm_eps, xn)
-                qkv = torch.empty(M, 3 * D, device=dev, dtype=e16)
-                K.gemm(xn, self._w(pre + "qkv", at.qkv.weight), M=M, N=3 * D, K=D, out=qkv,
-                       bias=self._wf(pre + "qkvb", at.qkv.bias))
-                ao = torch.empty(M, D, device=dev, dtype=e16)
-                K.vit_attention(qkv, ao, self._wf(pre + "rh", at.rel_pos_h), self._wf(pre + "rw", at.rel_pos_w),
-                                nseq=B, side=g, heads=heads)
-                K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=M, N=D, K=D, out=x,
-                       bias=self._wf(pre + "projb", at.proj.bias), residual=x)
-                del qkv, ao
+                K.vit_attention(qkv, ao, rh, rw, nseq=B, side=g, heads=heads)
+            K.gemm(ao, self._w(pre + "proj", at.proj.weight), M=M, N=D, K=D, out=x,
+                   bias=self._wf(pre + "projb", at.proj.bias), residual=x)
+            del qkv, ao
             K.layernorm_fwd(x, self._wf(pre + "ln2w", layer.layer_norm2.weight),
                             self._wf(pre + "ln2b", layer.layer_norm2.bias), cfg.layer_norm_eps, xn)
             K.gemm(xn, self._w(pre + "fc1", layer.mlp.lin1.weight), M=M, N=cfg.mlp_dim, K=D, out=mlp_h,

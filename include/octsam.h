@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 10
+#define OCTSAM_ABI_VERSION 11
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -137,9 +137,14 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
  * side = 64 (global layers, nseq = batch) or 14 (windowed layers, nseq = batch * 25 windows);
  * head_dim = 64 (vit-b / vit-l) or 80 (vit-h); fp16 = 1: IEEE half operands, else bf16.
  * softmax(q k^T / sqrt(head_dim) + rel_h + rel_w) v with fp32 statistics; the T x T bias is never
- * materialised. 16-B aligned operands. */
+ * materialised. 16-B aligned operands.
+ * grid = 0: windowed qkv / out are window-ordered (window_partition applied, padding rows present).
+ * grid > 0 (side 14 only): qkv / out are token-ordered [images * grid * grid, ...] (no window_partition),
+ * nseq = images * ceil(grid/14)^2; tokens past the grid read pad_row ([3*heads*head_dim], the qkv of a zero
+ * row, i.e. the qkv bias) and their outputs are not written (window_unpartition drops them). */
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
-                         int32_t side, int32_t heads, int32_t head_dim, int32_t fp16, void* stream);
+                         int32_t side, int32_t heads, int32_t head_dim, int32_t fp16, int32_t grid,
+                         const void* pad_row, void* stream);
 
 /* ---------------------------------------------------------------- element-wise / reductions / prompts */
 /* out[i] = alpha*a[i] + beta*b[b_period ? i % b_period : i]  (a or b may be NULL = 0); out2_f32 optional copy.

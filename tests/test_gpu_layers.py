@@ -140,6 +140,47 @@ def test_vit_attention_deterministic(cuda, side, nseq, hd):
     assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
+def _window_partition(x, grid, ws, pad):
+    """[B*grid*grid, C] token rows -> [B*nw*nw*ws*ws, C] window rows, padding rows = pad (hf:modeling_sam.py:900-929
+    pads with zeros after layer_norm1, so a padding row's qkv is the bias)."""
+    B = x.shape[0] // (grid * grid)
+    nw = (grid + ws - 1) // ws
+    xp = pad.view(1, 1, 1, -1).expand(B, nw * ws, nw * ws, x.shape[1]).clone()
+    xp[:, :grid, :grid] = x.view(B, grid, grid, -1)
+    return xp.view(B, nw, ws, nw, ws, -1).permute(0, 1, 3, 2, 4, 5).reshape(-1, x.shape[1])
+
+
+def _window_unpartition(xw, B, grid, ws):
+    nw = (grid + ws - 1) // ws
+    x = xw.view(B, nw, nw, ws, ws, -1).permute(0, 1, 3, 2, 4, 5).reshape(B, nw * ws, nw * ws, -1)
+    return x[:, :grid, :grid].reshape(B * grid * grid, -1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hd,heads", [(64, 12), (80, 4)])
+@pytest.mark.parametrize("grid,B", [(64, 2), (23, 3), (14, 1)])
+def test_vit_attention_token_ordered_windows(cuda, grid, B, hd, heads, dtype):
+    """Windowed attention on token-ordered qkv (grid > 0: the partition / unpartition and the padding tokens'
+    bias row inside the kernel) is bit-identical to the window-ordered launch on the explicitly partitioned
+    tensor (which test_vit_attention checks against fp32), including ragged grids (23 = 14 + 9) and a grid
+    with no padding (14)."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(grid * 7 + hd + B)
+    D = heads * hd
+    ws = 14
+    nw = (grid + ws - 1) // ws
+    qkv = (0.5 * torch.randn(B * grid * grid, 3 * D, generator=g)).to(cuda, dtype)
+    pad = (0.5 * torch.randn(3 * D, generator=g)).to(cuda, dtype)
+    Rh = (0.2 * torch.randn(2 * ws - 1, hd, generator=g)).to(cuda)
+    Rw = (0.2 * torch.randn(2 * ws - 1, hd, generator=g)).to(cuda)
+    qkv_w = _window_partition(qkv, grid, ws, pad)
+    out_w = torch.empty(qkv_w.shape[0], D, device=cuda, dtype=dtype)
+    kernels.vit_attention(qkv_w, out_w, Rh, Rw, nseq=B * nw * nw, side=ws, heads=heads)
+    out = torch.full((B * grid * grid, D), float("nan"), device=cuda, dtype=dtype)
+    kernels.vit_attention(qkv, out, Rh, Rw, nseq=B * nw * nw, side=ws, heads=heads, grid=grid, pad_row=pad)
+    assert torch.equal(out, _window_unpartition(out_w, B, grid, ws))
+
+
 def test_patchify_bf16(cuda):
     """Patch-embedding operand: rows (b, patch row, patch col), k = (c, ky, kx), bf16-rounded pixels."""
     from dilabhelmholtzoct_amd import kernels
