@@ -35,6 +35,7 @@ class GemmArgs(ctypes.Structure):
         ("a2_rows", c_int32), ("b2_rows", c_int32),
         ("a_blk", c_int32), ("a_rep", c_int32), ("b_blk", c_int32), ("b_rep", c_int32),
         ("r_blk", c_int32), ("r_rep", c_int32), ("k_total", c_int32), ("c_rows", c_int32),
+        ("a_colsum", c_void_p), ("b_colsum", c_void_p),
     ]
 
 

@@ -103,6 +103,8 @@ struct GemmK {
   int k_total;  // split-K over k-major operands: rows >= k_total (counted from batch 0) read as zero
   int fast_epi;  // 8-phase kernels: lean epilogue kind (0 = general; else 1 + FE bits, see epilogue_fast)
   int c_rows;    // rows of C (and R) when a row map scatters the output (fast epilogue range)
+  float* a_cs;   // k-major operands: per-batch column sums of A [batch][M] / B [batch][N] (or null)
+  float* b_cs;
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -465,6 +467,23 @@ __device__ __forceinline__ e16x8 frag_km(const char* img, int xb, int kb, int la
   return __builtin_bit_cast(e16x8, v);
 }
 
+// s + the sum of an MFMA operand fragment's 8 elements (4 v_dot2 with ones: exact products, fp32 sums). A
+// k-major fragment holds 8 consecutive k of one row, so summing it over a tile's K-steps gives that row's
+// column sum of the operand (a bias gradient) from registers the MFMAs already loaded.
+__device__ __forceinline__ float frag_sum(e16x8 v, float s) {
+  const e16x2 one = {(e16)1.0f, (e16)1.0f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const e16x2 pr = {v[2 * q], v[2 * q + 1]};
+#ifdef OCTSAM_GEMM_F16
+    s = __builtin_amdgcn_fdot2(pr, one, s, false);
+#else
+    s = __builtin_amdgcn_fdot2_f32_bf16(pr, one, s, false);
+#endif
+  }
+  return s;
+}
+
 // Fast epilogue: adjacent lanes trade one value with a DPP quad swap so each lane owns two adjacent
 // columns of one row (even lane: row m, cols n,n+1; odd lane: row m+1, cols n-1,n) and writes them with one
 // 4-B (e16x2) or 8-B (float2) store. Loads are hoisted ahead of the stores so a store never waits on an
@@ -638,11 +657,24 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x16)0.0f;
+  // fused column sums (k-major operands), one fragment per wave so no wave carries much more VALU than the
+  // others: on the tiles of column 0 wave (wm, wn) sums A fragment i = wn (rows wm*64 + wn*32 ..), on the tiles
+  // of row 0 waves wm < NJ sum B fragment j = wm (columns wn*BN/2 + wm*32 ..): every element once per batch
+  float csa = 0.0f, csb = 0.0f;
+  bool cs_a = false, cs_b = false;
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < total) issue(s);
   for (int g = 0; g < total; ++g) {
+    if constexpr (AKM || BKM) {
+      if (g % nk == 0) {
+        int bz, r0, c0;
+        tile_of(g / nk, bz, r0, c0);
+        cs_a = AKM && p.a_cs != nullptr && c0 == 0;
+        cs_b = BKM && p.b_cs != nullptr && wm < NJ && r0 == 0;
+      }
+    }
     // wait for stage g: leave the younger (NS-2) stages in flight
     const int ahead = min(NS - 2, total - 1 - g);
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL_PER_WAVE) : "memory");
@@ -671,10 +703,37 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = mma32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if constexpr (AKM) {
+        if (cs_a) csa = frag_sum(wn ? af[1] : af[0], csa);
+      }
+      if constexpr (BKM) {
+        if (cs_b) {
+          e16x8 f = bfr[0];
+#pragma unroll
+          for (int j = 1; j < NJ; ++j) f = wm == j ? bfr[j] : f;
+          csb = frag_sum(f, csb);
+        }
+      }
     }
     if (g % nk == nk - 1) {
       int bz, r0, c0;
       tile_of(g / nk, bz, r0, c0);
+      if constexpr (AKM) {
+        if (cs_a) {  // lanes l and l + 32 hold the two k halves of row (l & 31)
+          const float v = csa + __shfl_xor(csa, 32, 64);
+          const int m = r0 + wm * 64 + wn * 32 + lane;
+          if (lane < 32 && m < p.M) p.a_cs[(long long)bz * p.M + m] = v;
+          csa = 0.0f;
+        }
+      }
+      if constexpr (BKM) {
+        if (cs_b) {
+          const float v = csb + __shfl_xor(csb, 32, 64);
+          const int n = c0 + wn * (BN_ / 2) + wm * 32 + lane;
+          if (lane < 32 && n < p.N) p.b_cs[(long long)bz * p.N + n] = v;
+          csb = 0.0f;
+        }
+      }
       epilogue_fast<2, NJ, LATE>(p, acc, bz, r0 + wm * 64, c0 + wn * (BN_ / 2), lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -2119,6 +2178,10 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
   k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
   k.k_total = a->k_total;
+  k.a_cs = a->a_colsum;
+  k.b_cs = a->b_colsum;
+  const bool want_cs = a->a_colsum != nullptr || a->b_colsum != nullptr;
+  OCTSAM_CHECK_ARG(!want_cs || (a->a_mode == 1 && a->b_mode == 1), "octsam_gemm: a_colsum / b_colsum need a_mode = b_mode = 1");
   {  // lean epilogue kind (epilogue_fast): no C_pre; a residual must have C's type, no broadcast (r_blk)
     const int es = a->c_f32 ? 4 : 2;
     const bool res_ok = a->R == nullptr || (a->r_f32 == a->c_f32 && (a->r_blk == 0 || a->row_map == nullptr) &&
@@ -2148,7 +2211,7 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   {
     const long long t64 = (long long)((a->M + 63) / 64) * ((a->N + 63) / 64) * a->batch;
     const long long t256 = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
-    if (am <= 1 && bm <= 1 && a->a_blk == 0 && a->b_blk == 0 && t256 < 96 && t64 <= 4096 && g_small) {
+    if (am <= 1 && bm <= 1 && a->a_blk == 0 && a->b_blk == 0 && t256 < 96 && t64 <= 4096 && g_small && !want_cs) {
       t_last_path = 3;
       if (am == 0 && bm == 0) return launch<0, 0, 64>(k, a->batch, s);
       if (am == 0 && bm == 1) return launch<0, 1, 64>(k, a->batch, s);
@@ -2208,6 +2271,8 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
     }
     return launch_glds<256, 64, 2>(k, a, s);
   }
+  OCTSAM_CHECK_ARG(!want_cs, "octsam_gemm: a_colsum / b_colsum need the LDS-DMA k-major path (16-B aligned operands, "
+                             "K %% 64 == 0 or a k_total tail, enough tiles)");
   t_last_path = 0;
   OCTSAM_CHECK_ARG(a->k_total == 0 || (am == 1 && bm == 1), "octsam_gemm: k_total needs a_mode = b_mode = 1");
   if (am == 0 && bm == 0) return launch<0, 0>(k, a->batch, s);

@@ -292,10 +292,14 @@ class MaskDecoder(nn.Module):
                 break
         return best, Mtok // best
 
-    def _dw(self, dy, x, M, out, *, ldy=None, ldx=None, x_add=None, x_add_rows=0, split=None, accumulate=False):
+    def _dw(self, dy, x, M, out, *, ldy=None, ldx=None, x_add=None, x_add_rows=0, split=None, accumulate=False,
+            db=None, dbx=None, dbx_fold=1):
         """out[o, i] (+)= sum_m dy[m, o] * (x[m, i] (+ x_add[m % rows, i])) -> fp32 (deterministic split-K).
         The periodic addend (the image PE added to the keys) is folded as dy^T x + S^T x_add with
-        S[p] = sum_j dy[j*rows + p], so the big product is a plain k-major GEMM."""
+        S[p] = sum_j dy[j*rows + p], so the big product is a plain k-major GEMM.
+        db (optional, fp32 [O]) = sum_m dy[m, o] and dbx (fp32 [I / dbx_fold]) = sum_m x[m, i] folded over
+        dbx_fold column groups: the bias gradients, summed inside the GEMM's pass over dy / x (image-side
+        weight gradients; both overwrite)."""
         O, I = out.shape
         ldy = O if ldy is None else ldy
         ldx = I if ldx is None else ldx
@@ -303,7 +307,7 @@ class MaskDecoder(nn.Module):
             rows = x_add_rows
             S = torch.empty(rows, O, device=out.device, dtype=torch.bfloat16)
             K.group_sum(dy, S, ld_in=ldy, cols=O, groups=1, nper=M // rows, rows_per=rows)
-            self._dw(dy, x, M, out, ldy=ldy, ldx=ldx, accumulate=accumulate)
+            self._dw(dy, x, M, out, ldy=ldy, ldx=ldx, accumulate=accumulate, db=db, dbx=dbx, dbx_fold=dbx_fold)
             self._dw(S, x_add, rows, out, ldy=O, ldx=ldx, accumulate=True)
             return out
         if split is None:
@@ -311,21 +315,30 @@ class MaskDecoder(nn.Module):
         else:
             Ks = M // split
         beta = 1.0 if accumulate else 0.0
+        dev = out.device
+        pa = torch.empty((split, O), device=dev, dtype=torch.float32) if db is not None else None
+        pb = torch.empty((split, I), device=dev, dtype=torch.float32) if dbx is not None else None
         if split == 1 and Ks == M:
-            K.gemm(dy, x, M=O, N=I, K=M, out=out, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, beta=beta)
-            return out
-        part = torch.empty((split, O, I), device=out.device, dtype=torch.float32)
-        K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, batch=split,
-               stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I, k_total=M if Ks * split != M else 0)
-        K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
+            K.gemm(dy, x, M=O, N=I, K=M, out=out, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, beta=beta,
+                   a_colsum=pa, b_colsum=pb)
+        else:
+            part = torch.empty((split, O, I), device=dev, dtype=torch.float32)
+            K.gemm(dy, x, M=O, N=I, K=Ks, out=part, a_mode=1, b_mode=1, lda=ldy, ldb=ldx, batch=split,
+                   stride_a=Ks * ldy, stride_b=Ks * ldx, stride_c=O * I, k_total=M if Ks * split != M else 0,
+                   a_colsum=pa, b_colsum=pb)
+            K.splitk_reduce(part.view(split, -1), out, split, beta=beta)
+        if pa is not None:
+            K.splitk_reduce(pa, db, split)
+        if pb is not None:
+            K.splitk_reduce(pb.view(split * dbx_fold, -1), dbx, split * dbx_fold)
         return out
 
-    def _dw_pe(self, dy, x, M, out, n_pe, pe_b):
+    def _dw_pe(self, dy, x, M, out, n_pe, pe_b, db=None):
         """Weight gradient of _proj_pe: out[o, i] = sum_m dy[m, o] x[m, i] for every grouped row o (one
         k-major GEMM over the M rows), plus sum_p S[p, o] pe[p, i] for the first n_pe rows, S[p] = sum_j
-        dy[j*4096 + p] (the PE term)."""
+        dy[j*4096 + p] (the PE term); db (optional) = sum_m dy[m, o], fused into the GEMM."""
         O = out.shape[0]
-        self._dw(dy, x, M, out, ldy=O)
+        self._dw(dy, x, M, out, ldy=O, db=db)
         S = torch.empty(L_IMG, n_pe, device=out.device, dtype=torch.bfloat16)
         K.group_sum(dy, S, ld_in=O, cols=n_pe, groups=1, nper=M // L_IMG, rows_per=L_IMG)
         self._dw(S, pe_b, L_IMG, out[:n_pe], ldy=n_pe, accumulate=True)
@@ -358,8 +371,11 @@ class MaskDecoder(nn.Module):
         ldy = O if ldy is None else ldy
         if dx_out is not None:
             self._dx(dy_b, w, M, dx_out, ldy=ldy, beta=dx_beta, ldc=ldc)
-        self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
         gb = self.G(bname) if bgroup is None else self._group(self.flat_grad, bgroup, 0)
+        if M >= 65536 and db_src is None:  # image side: the bias gradient rides on the weight gradient's pass
+            self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows, db=gb)
+            return
+        self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
         src = dy_b if db_src is None else db_src
         if ldy == O or db_src is not None:
             K.colsum(src, M, O, gb)
@@ -576,8 +592,9 @@ class MaskDecoder(nn.Module):
         # read-modify-written by each block's projection backward and read by LayerNorm4's backward per block
         dkeys = torch.empty(RL, C, device=dev, dtype=b16)
         K.gemm(dup1pre, self.W("upscale_conv1.weight"), M=RL, N=C, K=256, out=dkeys, b_mode=0)
-        self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256)
-        K.colsum(dup1pre, RL * 4, 64, self.G("upscale_conv1.bias"))
+        # (bias: column sums of dup1pre's [RL, 4 x 64] view, folded over the 4 ConvT taps)
+        self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256,
+                 dbx=self.G("upscale_conv1.bias"), dbx_fold=4)
         # ---- hypernetwork MLP backward -> dq7
         dq7 = torch.zeros(R, C, device=dev, dtype=f32)
         dq7v = dq7.view(P, T, C)
@@ -610,8 +627,7 @@ class MaskDecoder(nn.Module):
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
         self._dx(dKV, wkv, RL, dkeys, beta=1.0)
         self._dw_pe(dKV, s.keys2_b, RL, self._group(self.flat_grad, [f + "k_proj.weight", f + "v_proj.weight"], C),
-                    CI, s.pe_b)
-        K.colsum(dKV, RL, 2 * CI, self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
+                    CI, s.pe_b, db=self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
         # ---- two-way blocks in reverse
         for li in reversed(range(cfg.num_hidden_layers)):
             ls = s.layers[li]
@@ -674,19 +690,17 @@ class MaskDecoder(nn.Module):
                 K.group_sum(dKV0, dK_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 K.group_sum(dKV0[:, CI:], dV_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 K.group_sum(dQp, dQ_img, ld_in=CI, cols=CI, groups=B, nper=N, rows_per=L)
-                self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), x_add=s.pe_b, x_add_rows=L)
-                self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L)
-                self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"))
-                K.colsum(dK_img, Mi, CI, self.G(t2i + "k_proj.bias"))
-                K.colsum(dQ_img, Mi, CI, self.G(i2t + "q_proj.bias"))
-                K.colsum(dV_img, Mi, CI, self.G(t2i + "v_proj.bias"))
+                self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), x_add=s.pe_b, x_add_rows=L,
+                         db=self.G(t2i + "k_proj.bias"))
+                self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L,
+                         db=self.G(i2t + "q_proj.bias"))
+                self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"), db=self.G(t2i + "v_proj.bias"))
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
                 self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)
                 self._dw_pe(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq + [t2i + "v_proj.weight"], C),
-                            2 * CI, s.pe_b)
-                K.colsum(dKQV, RL, 3 * CI, self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",
-                                                                        t2i + "v_proj.bias"], 0))
+                            2 * CI, s.pe_b, db=self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",
+                                                                            t2i + "v_proj.bias"], 0))
                 dkeys = dkeys_in
             # LN1 / self attention
             dq, ds_b = self._ln_bwd(dq, ls.ln1)

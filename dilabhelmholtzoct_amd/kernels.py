@@ -24,10 +24,15 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
          stride_a: int = 0, stride_b: int = 0, stride_c: int = 0, stride_r: int = 0,
          A2: torch.Tensor | None = None, B2: torch.Tensor | None = None, a2_rows: int = 0,
          b2_rows: int = 0, conv_c: int = 0, a_remap: tuple[int, int] = (0, 1),
-         b_remap: tuple[int, int] = (0, 1), r_remap: tuple[int, int] = (0, 1), k_total: int = 0) -> torch.Tensor:
+         b_remap: tuple[int, int] = (0, 1), r_remap: tuple[int, int] = (0, 1), k_total: int = 0,
+         a_colsum: torch.Tensor | None = None, b_colsum: torch.Tensor | None = None) -> torch.Tensor:
     """C[b] = epi(alpha * A[b] @ B[b]^T); see octsam_gemm in include/octsam.h. The 16-bit operand type (bf16 or
-    fp16: octsam_gemm_f16) is B's; every other 16-bit operand must match it."""
-    _require_cuda(A, B, out, bias, residual, pre_out, row_map, A2, B2)
+    fp16: octsam_gemm_f16) is B's; every other 16-bit operand must match it. a_colsum / b_colsum (fp32
+    [batch, M] / [batch, N], k-major operands only): per-batch column sums of A / B, fused."""
+    _require_cuda(A, B, out, bias, residual, pre_out, row_map, A2, B2, a_colsum, b_colsum)
+    for name, t, n in (("a_colsum", a_colsum, M), ("b_colsum", b_colsum, N)):
+        if t is not None and (t.dtype != torch.float32 or t.numel() < batch * n or not t.is_contiguous()):
+            raise ValueError(f"{name} must be contiguous fp32 with batch * {n} elements")
     e16 = B.dtype
     if e16 not in (torch.bfloat16, torch.float16):
         raise ValueError(f"B must be bf16 or fp16, got {e16}")
@@ -57,7 +62,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         pre_f32=int(pre_out is not None and pre_out.dtype == torch.float32),
         conv_c=conv_c, a2_rows=a2_rows, b2_rows=b2_rows, a_blk=a_remap[0], a_rep=a_remap[1],
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
-        c_rows=min(out.numel() // ldc, 2 ** 31 - 1) if row_map is not None else 0)
+        c_rows=min(out.numel() // ldc, 2 ** 31 - 1) if row_map is not None else 0,
+        a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 11
+#define OCTSAM_ABI_VERSION 12
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -78,6 +78,12 @@ typedef struct octsam_gemm_args {
   /* rows of C (and R) when row_map scatters the output; lets the 256x256 kernels use their lean epilogue
      (byte offsets range-checked against c_rows * ldc); 0 = unknown (general epilogue) */
   int32_t c_rows;
+  /* column sums of the k-major operands (a_mode = b_mode = 1 only; fp32, NULL = none):
+     a_colsum[b*M + m] = sum_k A[b][k][m], b_colsum[b*N + n] = sum_k B[b][k][n] per batch b (split), i.e. the
+     bias gradient of a weight-gradient GEMM dW = dY^T X (A = dY), fused into the pass that reads dY; combine
+     the splits with octsam_splitk_reduce. */
+  float* a_colsum;
+  float* b_colsum;
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);

@@ -30,8 +30,13 @@ def t(fn, it=20):
 # (the windowed projection through the window -> token row map)
 SHAPES = [("qkv_win", 39200, 2304, 768, 0, 0), ("qkv_glob", 32768, 2304, 768, 0, 0),
           ("proj_win", 39200, 768, 768, 0, 2), ("proj", 32768, 768, 768, 0, 1), ("fc1", 32768, 3072, 768, 2, 0),
-          ("fc2", 32768, 768, 3072, 0, 1), ("dec_out", 688128, 256, 128, 0, 3), ("dec_kqv", 688128, 384, 256, 0, 4)]
+          ("fc2", 32768, 768, 3072, 0, 1), ("dec_out", 688128, 256, 128, 0, 3), ("dec_kqv", 688128, 384, 256, 0, 4),
+          ("sq8k", 8192, 8192, 8192, 0, 0), ("deep", 32768, 2304, 6144, 0, 0)]
+PICK = [x for x in os.environ.get("GEMM_SHAPES", "").split(",") if x]
+VPICK = [x for x in os.environ.get("GEMM_VARIANTS", "").split(",") if x]
 for name, M, N, Kd, act, res in SHAPES:
+    if PICK and name not in PICK:
+        continue
     A = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
     W = (torch.randn(N, Kd, device="cuda") / Kd ** 0.5).to(torch.bfloat16)
     bias = torch.randn(N, device="cuda")
@@ -54,6 +59,8 @@ for name, M, N, Kd, act, res in SHAPES:
     row = {"name": name, "M": M, "N": N, "K": Kd}
     variants = [("default", 1), ("single", 11), ("relax", 13), ("p1tile", 14), ("p_nostore", 16), ("p_tile0", 17),
                 ("general", 18), ("nopersist", 20), ("no192", 21), ("noepi", 6), ("noloop", 7), ("blaslt", None)]
+    if VPICK:
+        variants = [v for v in variants if v[0] in VPICK]
     best = {}
     for rnd in range(3):  # round-robin, min over rounds: no variant always runs first after a clock ramp
         for tag, fast in variants:

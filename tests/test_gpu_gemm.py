@@ -364,6 +364,57 @@ def test_dw_ragged_splitk(cuda, Mtok, O, I):
     assert _rel(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("Mrows,O,I,ragged", [(32768, 384, 256, False), (65536 + 640, 256, 128, True),
+                                               (32768, 128, 256, False), (24576, 200, 136, True)])
+@pytest.mark.parametrize("f16", [False, True])
+def test_dw_fused_colsums(cuda, Mrows, O, I, ragged, f16):
+    """Weight gradient with the bias gradients fused (a_colsum = sum_m dy[m, o], b_colsum = sum_m x[m, i]):
+    dW unchanged bit for bit against the same GEMM without them, the sums against fp32 column sums of the same
+    16-bit values (incl. a split-K tail zero-filled through k_total, ragged O / I, both 16-bit types)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    dt = torch.float16 if f16 else torch.bfloat16
+    g = torch.Generator().manual_seed(Mrows + O + I + f16)
+    dy = torch.randn(Mrows, O, generator=g).to(cuda, dt)
+    x = torch.randn(Mrows, I, generator=g).to(cuda, dt)
+    ks = 512 if not ragged else 576
+    split = -(-Mrows // ks)
+    kt = Mrows if split * ks != Mrows else 0
+    if kt:  # the operands must hold split * ks rows; the tail rows are never read
+        pad = split * ks - Mrows
+        dy = torch.cat([dy, torch.full((pad, O), float("nan"), device=cuda, dtype=dt)])
+        x = torch.cat([x, torch.full((pad, I), float("nan"), device=cuda, dtype=dt)])
+    outs, paths = [], []
+    pa = torch.empty(split, O, device=cuda)
+    pb = torch.empty(split, I, device=cuda)
+    for cs in (False, True):
+        part = torch.empty(split, O, I, device=cuda)
+        kernels.gemm(dy, x, M=O, N=I, K=ks, out=part, a_mode=1, b_mode=1, lda=O, ldb=I, batch=split,
+                     stride_a=ks * O, stride_b=ks * I, stride_c=O * I, k_total=kt,
+                     a_colsum=pa if cs else None, b_colsum=pb if cs else None)
+        paths.append(lib.octsam_gemm_last_path())
+        outs.append(part)
+    assert paths[1] == 1  # the sums force the LDS-DMA k-major kernel (few tiles would take the small path)
+    if paths[0] == 1:
+        assert torch.equal(outs[0], outs[1])
+    else:
+        assert _rel(outs[1], outs[0]) < 1e-5
+    ref_a = dy[:Mrows].float().sum(0)
+    ref_b = x[:Mrows].float().sum(0)
+    assert _rel(pa.sum(0), ref_a) < 1e-5 and _rel(pb.sum(0), ref_b) < 1e-5
+    per_split = dy[:Mrows].float()
+    assert _rel(pa[0], per_split[:ks].sum(0)) < 1e-5
+
+
+def test_dw_colsum_needs_kmajor_path(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    from dilabhelmholtzoct_amd._lib import OctsamError
+    A = torch.randn(256, 256, device=cuda).to(torch.bfloat16)
+    out = torch.empty(256, 256, device=cuda)
+    with pytest.raises(OctsamError, match="a_mode = b_mode = 1"):
+        kernels.gemm(A, A, M=256, N=256, K=256, out=out, a_colsum=torch.empty(256, device=cuda))
+
+
 @pytest.mark.parametrize("a_mode,b_mode", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("shape", [(1120, 256, 256, 1), (160, 32, 256, 1), (256, 256, 64, 18), (72, 200, 136, 3)])
 def test_gemm_small_path(cuda, a_mode, b_mode, shape):
