@@ -82,6 +82,14 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Workgroup id -> logical id so each XCD runs a contiguous range of logical ids: the dispatcher deals
+// workgroups to the 8 XCDs round-robin by linear id, which would put the workgroups that share K/V (the query
+// blocks of one (sequence, head)) on different XCDs, each fetching them into its own L2.
+__device__ __forceinline__ int xcd_logical(int id, int n) {
+  const int q = n >> 3, rr = n & 7, xcd = id & 7, loc = id >> 3;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+}
+
 template <int N> __device__ __forceinline__ void wait_vm();
 template <> __device__ __forceinline__ void wait_vm<0>() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 template <> __device__ __forceinline__ void wait_vm<2>() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
@@ -294,10 +302,12 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
   static_assert(NW * G_SCR * 4 <= G_RELH + NBUF * G::TILE, "rel_w scratch must fit");
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int head = blockIdx.y, seq = blockIdx.z;
+  // logical id = (seq, head, query block), query block fastest: the 16 blocks of a (seq, head) on one XCD
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int qblk = lid & 15, head = (lid >> 4) % heads, seq = (lid >> 4) / heads;
   const int D = heads * HD, ld = 3 * D;
   const E* base = qkv + (long long)seq * T * ld;
-  const int q = blockIdx.x * (NW * 32) + wave * 32 + l32;
+  const int q = qblk * (NW * 32) + wave * 32 + l32;
   const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
   const float c1 = scale * L2E;
   if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the SIMD's 2 waves drift
@@ -421,11 +431,13 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   float* scr = (float*)(wsm + 2 * G::TILE) + (threadIdx.x >> 6) * W_SCR;
   char* zero = wsm + NBUF * G::TILE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  // block x = (head, query half) fastest: the 2*heads workgroups of a window read the same qkv rows together
-  const int head = blockIdx.x >> 1, win = blockIdx.y;
+  // logical id = (window, head, query half), half fastest, dealt to XCDs in contiguous ranges: the 2*heads
+  // workgroups of a window read the same qkv rows through one L2
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int head = (lid >> 1) % heads, win = (lid >> 1) / heads, qhalf = lid & 1;
   const int D = heads * HD, ld = 3 * D;
   const WinRows<E> wr(qkv, pad, win, ld, grid);
-  const int q = (blockIdx.x & 1) * (WNW * 32) + wave * 32 + l32;
+  const int q = qhalf * (WNW * 32) + wave * 32 + l32;
   const int qc = q < T ? q : T - 1;
   const bool qvalid = q < T && wr.real(q);
   // the second workgroup's last wave (query slots 224..255) has no real query: it skips the rel tables and
@@ -546,7 +558,8 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
                                 g_smem<HD>());
       attr = true;
     }
-    hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(4096 / (NW * 32), heads, nseq), dim3(THR), g_smem<HD>(),
+    static_assert(4096 / (NW * 32) == 16, "16 query blocks per (sequence, head)");
+    hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(),
                        s, (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
   } else {
     static bool attr = false;
@@ -555,7 +568,7 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
                                 w_smem<HD>());
       attr = true;
     }
-    hipLaunchKernelGGL((vit_attn_window_kernel<HD, E>), dim3(2 * heads, nseq, 1), dim3(WTHR), w_smem<HD>(), s,
+    hipLaunchKernelGGL((vit_attn_window_kernel<HD, E>), dim3(2 * heads * nseq), dim3(WTHR), w_smem<HD>(), s,
                        (const E*)qkv, (E*)out, Rh, Rw, heads, scale, grid, (const E*)pad);
   }
   return 0;
