@@ -106,6 +106,42 @@ __device__ __forceinline__ typename ET<E>::v8 pack8(const f32x16& a, int base) {
 
 // 32 table rows j0 .. j0+31 of P^T = R . Q^T for the lane's query (natural units), rows outside [0, nrows)
 // zero. R fp32 [nrows][HD], rounded to the element type like the q.k operands.
+// Split form for prologues that issue the K/V DMA after the table rows: rel_load fetches the lane's table row
+// (rows outside [0, nrows) clamped, zeroed by rel_mma), so the compiler's counted wait for it does not cover
+// DMA issued later.
+template <int HD> struct RelRow {
+  float4 x[Geo<HD>::NKS][2];
+};
+template <int HD>
+__device__ __forceinline__ RelRow<HD> rel_load(const float* __restrict__ R, int j0, int nrows, int lane) {
+  const int h = lane >> 5, j = min(max(j0 + (lane & 31), 0), nrows - 1);
+  RelRow<HD> r;
+#pragma unroll
+  for (int s = 0; s < Geo<HD>::NKS; ++s) {
+    const float* rp = R + j * HD + 16 * s + 8 * h;
+    r.x[s][0] = *(const float4*)rp;
+    r.x[s][1] = *(const float4*)(rp + 4);
+  }
+  return r;
+}
+template <int HD, typename E>
+__device__ __forceinline__ f32x16 rel_mma(const RelRow<HD>& rr, int j0, int nrows,
+                                          const typename ET<E>::v8 (&qf)[Geo<HD>::NKS], int lane) {
+  const int j = j0 + (lane & 31);
+  const bool ok = j >= 0 && j < nrows;
+  f32x16 acc = (f32x16)0.0f;
+#pragma unroll
+  for (int s = 0; s < Geo<HD>::NKS; ++s) {
+    const float4 x0 = rr.x[s][0], x1 = rr.x[s][1];
+    typename ET<E>::v8 a;
+    a[0] = (E)x0.x; a[1] = (E)x0.y; a[2] = (E)x0.z; a[3] = (E)x0.w;
+    a[4] = (E)x1.x; a[5] = (E)x1.y; a[6] = (E)x1.z; a[7] = (E)x1.w;
+    if (!ok) a = (typename ET<E>::v8)(E)0.0f;
+    acc = ET<E>::mma(a, qf[s], acc);
+  }
+  return acc;
+}
+
 template <int HD, typename E>
 __device__ __forceinline__ f32x16 rel_block(const float* __restrict__ R, int j0, int nrows,
                                             const typename ET<E>::v8 (&qf)[Geo<HD>::NKS], int lane) {
@@ -419,7 +455,7 @@ static_assert(WNW * W_SCR * 4 <= Geo<64>::TILE, "rel-table scratch must fit in o
 static_assert(w_smem<64>() <= 160 * 1024 / 3, "three windowed workgroups per CU at head_dim 64");
 
 template <int HD, typename E>
-__global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+__global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel(const E* __restrict__ qkv, E* __restrict__ out,
                                                               const float* __restrict__ Rh,
                                                               const float* __restrict__ Rw, int heads, float scale,
                                                               int grid, const E* __restrict__ pad) {
@@ -446,8 +482,12 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
   const int qh = qc / S, qw = qc % S;
   const float c1 = scale * L2E;
 
+  // Q and both tables' rows first, the K/V DMA after them: the waits for Q and the tables then leave the
+  // DMA in flight (vmcnt retires in issue order)
   V8 qf[G::NKS];
   load_q<HD, E>(wr.at(qc) + head * HD, qf, h);
+  const RelRow<HD> rw_rows = rel_load<HD>(Rw, 0, 2 * S - 1, lane);
+  const RelRow<HD> rh_rows = rel_load<HD>(Rh, 0, 2 * S - 1, lane);
   const int koff = D + head * HD, voff = 2 * D + head * HD;
   load_tile_win<HD, WNW, E>(wr, koff, voff, 0, ring, wave, lane);
   load_tile_win<HD, WNW, E>(wr, koff, voff, 64, ring + G::TILE, wave, lane);
@@ -459,7 +499,7 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
 #pragma unroll
   for (int i = 0; i < S; ++i) relh[i] = 0.0f;
   if (!idle) {
-    const f32x16 t = rel_block<HD, E>(Rw, 0, 2 * S - 1, qf, lane);
+    const f32x16 t = rel_mma<HD, E>(rw_rows, 0, 2 * S - 1, qf, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       if (acc_row(r, h) < 2 * S - 1) scr[acc_row(r, h) * 33 + l32] = t[r];
@@ -473,7 +513,7 @@ __global__ __launch_bounds__(WTHR, 2) void vit_attn_window_kernel(const E* __res
     }
   }
   if (!idle) {
-    const f32x16 t = rel_block<HD, E>(Rh, 0, 2 * S - 1, qf, lane);
+    const f32x16 t = rel_mma<HD, E>(rh_rows, 0, 2 * S - 1, qf, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       if (acc_row(r, h) < 2 * S - 1) scr[acc_row(r, h) * 33 + l32] = t[r];
