@@ -70,6 +70,9 @@ def parse():
                    help="time building one batch on the host (reference data path) vs the HIP data path")
     p.add_argument("--no-events", action="store_true", help="do not record per-kernel HIP events")
     p.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
+    p.add_argument("--pipeline", type=int, default=1,
+                   help="encoder lookahead (graph mode): the next step's frozen-encoder phase replays on a side "
+                        "stream during this step's decoder; every timed step still runs its own encoder")
     p.add_argument("--roof-steps", type=int, default=2, help="eager steps timed per GEMM launch for the roofline")
     p.add_argument("--e2e-steps", type=int, default=10,
                    help="steps of the end-to-end loop (a new batch per step through the HIP data path)")
@@ -308,13 +311,19 @@ def end_to_end(args, step, device, rank, world, pg, n_raw=4):
         return b, ev
 
     def run(n):
-        nxt = prep(0)
+        # batches are built two ahead (during step i: batch i + 2) so that step i can name batch i + 1 for the
+        # encoder lookahead; the last step names none (exactly n encoder passes)
+        ready = [prep(0), prep(1)]
         for i in range(n):
-            cur, ev = nxt
+            cur, ev = ready[0]
             main_stream.wait_event(ev)
+            nb = None
+            if i + 1 < n:
+                main_stream.wait_event(ready[1][1])
+                nb = ready[1][0]
             holder = []
-            step.step(cur, between=lambda i=i: holder.append(prep(i + 1)))
-            nxt = holder[0]
+            step.step(cur, between=lambda i=i: holder.append(prep(i + 2)), next_batch=nb)
+            ready = [ready[1], holder[0]]
         step.flush()
 
     log(f"rank {rank}: end-to-end warm-up (one capture per batch shape)")
@@ -354,13 +363,14 @@ def topo_all_sensitivity(args, model, batch, steps=5):
     """ms/step with the topo_mode='all' reading of torch_topological's batch_iter (every prompt's diagrams,
     2*B*N persistence maps per step instead of 2*B; SURVEY.md §8(a) A17 — the reading is unpinned)."""
     from dilabhelmholtzoct_amd.train import FusedTrainStep
-    st = FusedTrainStep(model, lr=1e-3, topological=True, topo_mode="all", graphs=not args.eager)
-    for _ in range(2):
-        st.step(batch)
+    pipe = bool(args.pipeline) and not args.eager
+    st = FusedTrainStep(model, lr=1e-3, topological=True, topo_mode="all", graphs=not args.eager, pipeline=pipe)
+    for i in range(2):
+        st.step(batch, next_batch=batch if i == 0 else None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        st.step(batch)
+    for i in range(steps):
+        st.step(batch, next_batch=batch if i + 1 < steps else None)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     B, N = batch["gt_u8"].shape[:2]
@@ -455,7 +465,9 @@ def main():
     model = SamModel.from_pretrained(args.model, seed=0).to(device)
     if args.dtype == "fp16":
         model.set_encoder_dtype(torch.float16)
-    step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager)
+    pipe = bool(args.pipeline) and not args.eager
+    step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager,
+                          pipeline=pipe)
 
     def barrier():
         if pg is not None:
@@ -464,15 +476,17 @@ def main():
         torch.cuda.synchronize()
 
     log(f"rank {rank}: N={N} prompts/image, warm-up")
-    for _ in range(args.warmup):
-        step.step(batch)
+    # with the encoder lookahead, the last step of each loop names no next batch: nothing of a timed step runs
+    # before the timer starts, and the timed region holds exactly `steps` encoder passes
+    for i in range(args.warmup):
+        step.step(batch, next_batch=batch if i + 1 < args.warmup else None)
     step.flush()
     barrier()
     log(f"rank {rank}: timing {args.steps} steps")
     t0 = time.perf_counter()
     loss = None
-    for _ in range(args.steps):
-        loss = step.step(batch)
+    for i in range(args.steps):
+        loss = step.step(batch, next_batch=batch if i + 1 < args.steps else None)
     step.flush()  # a deferred (overlapped) update belongs to the timed work
     barrier()
     dt = time.perf_counter() - t0
@@ -603,7 +617,10 @@ def main():
                     f"weights (seed 0)",
             "config": {"workload": workload_name(args), "model": args.model, "global_batch": args.batch * world,
                        "prompts_per_image": N, "prompt": args.prompt, "top": bool(args.top),
-                       "parallelism": f"dp{world}", "exec": "eager" if args.eager else "hipgraph"},
+                       "parallelism": f"dp{world}",
+                       "exec": "eager" if args.eager else
+                       ("hipgraph + encoder lookahead (next step's frozen encoder on a side stream during this "
+                        "step's decoder; each timed step runs its own encoder)" if pipe else "hipgraph")},
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
             "val_dice": val_dice,
             "val_metrics_mean": val_metrics,

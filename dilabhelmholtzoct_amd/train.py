@@ -33,8 +33,8 @@ class _Phases:
 class FusedTrainStep:
     """One training step of the reference (training_utils.py:46-69) as three phases:
 
-      E  encoder forward + prompt tokens              (reads no trainable weight)
-      F  decoder forward, post-processing, DiceCE fwd/bwd, topo-loss device forward (PH), D2H of the
+      E  image encoder forward                        (reads no trainable weight)
+      F  prompt tokens, decoder forward, post-processing, DiceCE fwd/bwd, topo-loss device forward (PH), D2H of the
          persistence pairs
       -- host: W2 between diagrams (POT emd2 restated) -> d topo / d map, topo loss
       B  H2D of the topo gradient, topo backward, post-processing backward, decoder backward
@@ -44,11 +44,20 @@ class FusedTrainStep:
     batch shape is seen, after eager warm-up, and replays them afterwards: no per-kernel host launch cost.
     In data-parallel runs (overlap=True) the all-reduce runs on a side stream and Adam is deferred to the
     next step, after that step's encoder forward has been queued: the gradient exchange overlaps the
-    encoder; flush() completes a pending update."""
+    encoder; flush() completes a pending update.
+
+    pipeline=True (graph mode): step(batch, next_batch=...) replays the encoder phase E of next_batch on a
+    side stream while this step's decoder phases F / F2 / B run, so the MFMA-bound frozen encoder fills the
+    CUs the HBM- and latency-bound decoder kernels leave idle. E reads no trainable weight, so the result is
+    the sequential one bit for bit. Two graph sets per batch shape (separate memory pools, the image
+    embedding double-buffered by set parity); the next step consumes the prefetched embedding if its inputs
+    are the tensors next_batch named (same storage and version), else it runs E itself. Every step still
+    runs its own E exactly once (the lookahead is the next step's E, moved earlier)."""
 
     def __init__(self, model: SamModel, lr: float = 1e-3, weight_decay: float = 0.0, topological: bool = False,
                  lamda: float = 0.1, interp: int = 50, betas=(0.9, 0.999), eps: float = 1e-8,
-                 topo_mode: str = "first", process_group=None, graphs: bool = False, overlap: bool = True):
+                 topo_mode: str = "first", process_group=None, graphs: bool = False, overlap: bool = True,
+                 pipeline: bool = False):
         self.model = model
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.topological, self.lamda, self.interp, self.topo_mode = topological, lamda, interp, topo_mode
@@ -63,6 +72,11 @@ class FusedTrainStep:
         self._graphs = {}       # batch shape -> captured graphs + static input copies (graph mode)
         self._pending = None    # (event, ) of an all-reduce whose Adam step has not run yet
         self._side = None
+        self.pipeline = pipeline and graphs
+        self._enc_stream = None
+        self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
+        self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
+        self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
 
     def image_pe(self):
         G = self.model.shared_image_embedding.positional_embedding
@@ -74,11 +88,13 @@ class FusedTrainStep:
     # ------------------------------------------------------------------ phases
     def _phase_e(self, st):
         st.emb = self.model.vision_encoder.forward_nhwc(st.pixel_values)
-        st.tokens = self.model.prompt_tokens(st.input_points, st.input_labels, st.input_boxes)
 
     def _phase_f(self, st, backward):
         model = self.model
         dec = model.mask_decoder
+        # the prompt tokens start with the decoder's iou / mask tokens (trainable): built here, after the
+        # previous step's Adam, not in E (which may run ahead of that update: DP overlap, pipelining)
+        st.tokens = model.prompt_tokens(st.input_points, st.input_labels, st.input_boxes)
         B, N = st.tokens.shape[:2]
         H, W = st.orig
         low, _, st.saved = dec.forward_impl(st.emb, self.image_pe(), st.tokens,
@@ -152,14 +168,15 @@ class FusedTrainStep:
 
     @torch.no_grad()
     def forward_backward(self, pixel_values, gt_u8, input_boxes=None, input_points=None, input_labels=None,
-                         crop=(992, 1024), orig=(496, 512), global_batch=None, backward=True, between=None):
+                         crop=(992, 1024), orig=(496, 512), global_batch=None, backward=True, between=None,
+                         next_inputs=None):
         """Returns a device float64 tensor [4] = (dice, ce, topo, total). With backward=True leaves the
         decoder gradient in mask_decoder.flat_grad. global_batch: images in the global (all-rank) batch,
         which fixes the topological loss's batch nesting. between: optional callable run on
         the host while the GPU works on the step (after the forward is queued)."""
         if self.graphs and backward:
             return self._graph_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop,
-                                                orig, global_batch, between)
+                                                orig, global_batch, between, next_inputs)
         out = self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                            global_batch, backward)
         if between is not None:
@@ -182,9 +199,34 @@ class FusedTrainStep:
 
     MAX_GRAPHS = 8  # captured step graphs kept (one per batch shape: B, the prompt count N, prompt kind)
 
-    def _capture(self, key, inputs, crop, orig, global_batch):
-        """Capture E / F / F2 / B for one batch shape. The graphs read their own static copies of the
-        inputs (``inputs`` is cloned), so any later batch of the same shape is replayed after a copy-in."""
+    def _encoder_set(self, ekey, pixel_values):
+        """Captured encoder graph E for one pixel shape and parity: its own memory pool, a static pixel input and
+        the image embedding it writes (read by every decoder graph set of that parity)."""
+        es = self._esets.get(ekey)
+        if es is not None:
+            return es
+        px = pixel_values.detach().to(pixel_values.device, copy=True)
+        st = _Phases()
+        st.pixel_values = px
+        ge = torch.cuda.CUDAGraph()
+        dev = px.device
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(ge, stream=s, capture_error_mode="relaxed"):
+                self._phase_e(st)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        es = {"graph": ge, "pixel": px, "emb": st.emb, "src": None, "e_done": torch.cuda.Event(),
+              "b_done": torch.cuda.Event()}
+        es["b_done"].record()
+        self._esets[ekey] = es
+        return es
+
+    def _capture(self, key, inputs, crop, orig, global_batch, ekey):
+        """Capture F / F2 / B for one batch shape (and E for its pixel shape if not captured yet). The graphs
+        read their own static copies of the inputs (``inputs`` is cloned), so any later batch of the same shape
+        is replayed after a copy-in."""
         dev = inputs[0].device
         # device copies (prompts may come as host tensors from the data path; the graphs read device memory)
         pixel_values, gt_u8, input_boxes, input_points, input_labels = (
@@ -193,7 +235,9 @@ class FusedTrainStep:
         self._eager_forward_backward(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                      global_batch, True)
         torch.cuda.synchronize()
-        st = self._state(pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch)
+        es = self._encoder_set(ekey, pixel_values)
+        st = self._state(es["pixel"], gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch)
+        st.emb = es["emb"]
         B, N = gt_u8.shape[:2]
         if self.topological and self.lamda != 0.0:
             entries, maps, midx = topo_index(B, N, self.topo_mode, global_batch, dev)
@@ -208,15 +252,13 @@ class FusedTrainStep:
         if st.pinned is None:  # no host phase: the pinned topo scalar stays 0
             st.pinned = ()
         st.topo_pinned = torch.zeros(1, dtype=torch.float64, pin_memory=True)
-        ge, gf, gf2, gb = (torch.cuda.CUDAGraph() for _ in range(4))
+        gf, gf2, gb = (torch.cuda.CUDAGraph() for _ in range(3))
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            with torch.cuda.graph(ge, stream=s, capture_error_mode="relaxed"):
-                self._phase_e(st)
-            pool = ge.pool()
-            with torch.cuda.graph(gf, stream=s, pool=pool, capture_error_mode="relaxed"):
+            with torch.cuda.graph(gf, stream=s, capture_error_mode="relaxed"):
                 self._phase_f(st, True)
+            pool = gf.pool()
             with torch.cuda.graph(gf2, stream=s, pool=pool, capture_error_mode="relaxed"):
                 self._phase_f2(st)
             with torch.cuda.graph(gb, stream=s, pool=pool, capture_error_mode="relaxed"):
@@ -226,8 +268,8 @@ class FusedTrainStep:
         if st.pinned == ():
             st.pinned = None
             st.topo_dev = None
-        static = (pixel_values, gt_u8, input_boxes, input_points, input_labels)
-        g = {"graphs": (ge, gf, gf2, gb), "st": st, "ev": torch.cuda.Event(), "static": static,
+        static = (None, gt_u8, input_boxes, input_points, input_labels)  # pixels: the encoder set's input
+        g = {"graphs": (gf, gf2, gb), "eset": es, "st": st, "ev": torch.cuda.Event(), "static": static,
              "src": tuple(self._src_tag(t) for t in inputs)}
         self._graphs[key] = g
         while len(self._graphs) > self.MAX_GRAPHS:
@@ -243,22 +285,45 @@ class FusedTrainStep:
         last and have not changed since: same storage, same version counter)."""
         tags = tuple(self._src_tag(t) for t in inputs)
         for dst, src, tag, old in zip(g["static"], inputs, tags, g["src"]):
-            if src is not None and tag != old:
+            if dst is not None and src is not None and tag != old:
                 dst.copy_(src, non_blocking=True)
         g["src"] = tags
 
+    @staticmethod
+    def _pixel_in(es, px):
+        tag = FusedTrainStep._src_tag(px)
+        if tag != es["src"]:
+            es["pixel"].copy_(px, non_blocking=True)
+            es["src"] = tag
+
     def _graph_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
-                                global_batch, between=None):
+                                global_batch, between=None, next_inputs=None):
         inputs = (pixel_values, gt_u8, input_boxes, input_points, input_labels)
         key = self._graph_key(*inputs) + (tuple(crop), tuple(orig), global_batch)
-        g = self._graphs.get(key)
+        ekey0 = (tuple(pixel_values.shape), pixel_values.dtype)
+        par = self._parity.get(ekey0, 0) if self.pipeline else 0
+        ekey = ekey0 + (par,)
+        g = self._graphs.get(key + (par,))
         if g is None:
-            g = self._capture(key, inputs, crop, orig, global_batch)
+            g = self._capture(key + (par,), inputs, crop, orig, global_batch, ekey)
             g["src"] = (None,) * 5  # the capture ran on clones: copy this batch in like any other
-        self._copy_in(g, inputs)
-        ge, gf, gf2, gb = g["graphs"]
+        es = g["eset"]
+        gf, gf2, gb = g["graphs"]
         st, ev = g["st"], g["ev"]
-        ge.replay()
+        main = torch.cuda.current_stream()
+        pre = self._prefetch
+        self._prefetch = None
+        if pre is not None and pre[0] is es and pre[1] == self._src_tag(pixel_values):
+            main.wait_event(es["e_done"])  # this batch's E ran ahead on the encoder stream
+        else:
+            if pre is not None:
+                main.wait_event(pre[0]["e_done"])  # a lookahead for other pixels: let it finish, then redo E
+            self._pixel_in(es, pixel_values)
+            es["graph"].replay()
+        self._copy_in(g, inputs)
+        if self.pipeline and next_inputs is not None:
+            # queued before the deferred update and F: the next E may also overlap a pending all-reduce
+            self._launch_lookahead(ekey0, par, next_inputs[0])
         self._finish_pending()
         gf.replay()
         if st.pinned is not None:
@@ -272,7 +337,35 @@ class FusedTrainStep:
         if st.pinned is not None:
             st.topo_pinned.numpy()[0] = loss
         gb.replay()
+        if self.pipeline:
+            es["b_done"].record(main)
+            self._parity[ekey0] = 1 - par
         return st.loss_out
+
+    def _launch_lookahead(self, ekey0, par, next_px):
+        """Replay E of the next batch's pixels on the encoder stream (encoder set of the other parity) once that
+        set's previous step (its B, which reads the embedding) has finished; the pixel copy-in runs on the same
+        stream. Any prompt count: only the pixel shape has to match."""
+        if (tuple(next_px.shape), next_px.dtype) != ekey0:
+            return  # another pixel shape: its first step runs E itself
+        es = self._esets.get(ekey0 + (1 - par,))
+        if es is None:
+            return  # the other set is captured when a step first needs it
+        main = torch.cuda.current_stream()
+        if self._enc_stream is None:
+            self._enc_stream = torch.cuda.Stream(device=main.device)
+        enc = self._enc_stream
+        enc.wait_event(es["b_done"])
+        ready = torch.cuda.Event()
+        ready.record(main)  # the next pixels were produced on (or handed to) the main stream
+        enc.wait_event(ready)
+        with torch.cuda.stream(enc):
+            self._pixel_in(es, next_px)
+            es["graph"].replay()
+            es["e_done"].record(enc)
+        if next_px.is_cuda:
+            next_px.record_stream(enc)
+        self._prefetch = (es, self._src_tag(next_px))
 
     @torch.no_grad()
     def allreduce_grads(self, n_local=None, n_global=None):
@@ -322,16 +415,21 @@ class FusedTrainStep:
         """Apply a deferred (overlapped) parameter update."""
         self._finish_pending()
 
-    def step(self, batch: dict, n_global=None, between=None):
+    def step(self, batch: dict, n_global=None, between=None, next_batch: dict | None = None):
         """batch: device tensors from data.process_batch/to_device_batch. n_global: images in the global
         batch (data parallel; None = this rank's batch is the whole batch). between: host work to overlap
-        with the step (see forward_backward)."""
+        with the step (see forward_backward). next_batch (pipeline=True): the batch the next step() gets; its
+        encoder phase runs during this step's decoder."""
         crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
         orig = tuple(int(v) for v in batch["original_sizes"][0])
         n_local = int(batch["pixel_values"].shape[0])
+        nxt = None
+        if next_batch is not None:
+            nxt = (next_batch["pixel_values"], next_batch["gt_u8"], next_batch.get("input_boxes"),
+                   next_batch.get("input_points"), next_batch.get("input_labels"))
         loss = self.forward_backward(batch["pixel_values"], batch["gt_u8"], input_boxes=batch.get("input_boxes"),
                                      input_points=batch.get("input_points"), input_labels=batch.get("input_labels"),
-                                     crop=crop, orig=orig, global_batch=n_global, between=between)
+                                     crop=crop, orig=orig, global_batch=n_global, between=between, next_inputs=nxt)
         self._launch_update(n_local, n_global)
         return loss
 
