@@ -621,30 +621,44 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     tds = data.SAMDataset(train_data, config, epoch_seed=config.get("data_seed"))
     vds = data.SAMDataset(valid_data, config, epoch_seed=config.get("data_seed"))
     bs = int(config.get("batch_size", 2))
+    # config "graphs" / "pipeline" (off by default): hipGraph replay per batch shape, and the encoder lookahead
+    # (the next batch is built before this step so its encoder can run during this step's decoder)
+    graphs = bool(config.get("graphs", False)) and device.type == "cuda"
     step = FusedTrainStep(model, lr=config.get("learning_rate", 1e-3), weight_decay=config.get("weight_decay", 0.0),
                           topological=bool(config.get("topological", False)),
-                          topo_mode=config.get("topo_mode", "first"), process_group=pg)
+                          topo_mode=config.get("topo_mode", "first"), process_group=pg, graphs=graphs,
+                          pipeline=graphs and bool(config.get("pipeline", False)))
     hist = {"train_loss": [], "valid_loss": []}
+
+    def build(bi, idx):
+        n_glob = len(tds) - bi * bs * world if bi == len(batches) - 1 else bs * world
+        n_glob = min(n_glob, bs * world)
+        prep = _prep(tds, idx, prompt, device, device_data)
+        N = _collective_max(prep[2], pg)
+        return n_glob, (_finish(prep, processor, prompt, N, device) if idx else None)
+
     for epoch in range(int(config.get("epochs", 10))):
         tds.epoch = epoch
         batches = global_batches(len(tds), bs, world, rank, bool(config.get("shuffle", False)),
                                  config.get("data_seed") or 0, epoch)
         epoch_loss = 0.0
+        nxt = build(1, batches[1]) if len(batches) > 1 else None
         for bi, idx in enumerate(batches):
             if bi == 0:  # training_utils.py:40-44: the first batch of every epoch is skipped
                 continue
-            n_glob = len(tds) - bi * bs * world if bi == len(batches) - 1 else bs * world
-            n_glob = min(n_glob, bs * world)
-            prep = _prep(tds, idx, prompt, device, device_data)
-            N = _collective_max(prep[2], pg)
+            n_glob, batch = nxt
+            # same batch order and RNG draws as building each batch at its own step (the builds stay in order)
+            nxt = build(bi + 1, batches[bi + 1]) if bi + 1 < len(batches) else None
             if idx:
-                batch = _finish(prep, processor, prompt, N, device)
                 crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
                 orig = tuple(int(v) for v in batch["original_sizes"][0])
+                nb = nxt[1] if (nxt is not None and step.pipeline) else None
+                nxt_in = None if nb is None else (nb["pixel_values"], nb["gt_u8"], nb.get("input_boxes"),
+                                                  nb.get("input_points"), nb.get("input_labels"))
                 loss = step.forward_backward(batch["pixel_values"], batch["gt_u8"],
                                              input_boxes=batch.get("input_boxes"),
                                              input_points=batch.get("input_points"), crop=crop, orig=orig,
-                                             global_batch=n_glob)
+                                             global_batch=n_glob, next_inputs=nxt_in)
                 lv = loss[3].double().cpu() * len(idx)
             else:  # nothing on this rank in a ragged last batch: contribute zero gradient
                 model.mask_decoder.flat_grad.zero_()

@@ -13,14 +13,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run(cuda, gpu_processor, gpu_components, data_seed, prompt="bboxes"):
+def _run(cuda, gpu_processor, gpu_components, data_seed, prompt="bboxes", **extra):
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.train import training
     np.random.seed(123)
     random.seed(123)
     cfg = {"batch_size": 2, "epochs": 1, "learning_rate": 1e-3, "topological": True, "prompt_type": prompt,
            "evaluate": True, "checkpoint": None, "data_seed": data_seed, "gpu_processor": gpu_processor,
-           "gpu_components": gpu_components}
+           "gpu_components": gpu_components, **extra}
     return training("facebook/sam-vit-base", cfg, data.synthetic_oct(seed=0, n=6), data.synthetic_oct(seed=1, n=2),
                     device=cuda)
 
@@ -39,3 +39,20 @@ def test_training_loop_host_vs_device_data_path(cuda, data_seed, prompt):
     for name in ("hip processor", "hip data path"):
         for key in ("train_loss", "valid_loss", "mean_dice", "dice"):
             assert runs[name][key] == ref[key], (name, key)
+
+
+def test_training_loop_graphs_and_lookahead(cuda):
+    """config graphs / pipeline: hipGraph replay and the encoder lookahead (the next batch built one step ahead)
+    give the eager loop's numbers exactly (6 scans -> 2 steps per epoch after the skip, 2 epochs)."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.train import training
+    out = []
+    for extra in ({}, {"graphs": True, "pipeline": True}):
+        np.random.seed(123)
+        random.seed(123)
+        cfg = {"batch_size": 2, "epochs": 2, "learning_rate": 1e-3, "topological": True, "prompt_type": "bboxes",
+               "evaluate": True, "checkpoint": None, "data_seed": 0, **extra}
+        out.append(training("facebook/sam-vit-base", cfg, data.synthetic_oct(seed=0, n=6),
+                            data.synthetic_oct(seed=1, n=2), device=cuda))
+    for key in ("train_loss", "valid_loss", "mean_dice", "dice"):
+        assert out[0][key] == out[1][key], key
