@@ -2252,8 +2252,13 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // next tile there anyway, and the tile's load latency still overlaps the epilogue)
       const bool res_small_k =
           a->R != nullptr && k.fast_epi == 11 && a->K <= 512 && a->act == 0;  // (kind 3 measured slower)
-      const bool persist = (a->R == nullptr || res_small_k) && a->row_map == nullptr && a->N <= ph8::BIAS_MAX &&
-                           g_use_glds != 11 && g_use_glds != 20 &&
+      // bias / activation kinds (encoder QKV, MLP1) run one tile per workgroup by default: under the encoder
+      // lookahead (train.FusedTrainStep pipeline) the decoder's kernels share the chip, and hardware-scheduled
+      // workgroups fill the CUs they leave while a fixed persistent grid waits for all of them (same-process
+      // A/B: 18.2 -> 17.7 ms/step); fast path 23 (and the 12..17 diagnostics) keep them persistent
+      const bool persist_bias = g_use_glds == 23 || (g_use_glds >= 12 && g_use_glds <= 17);
+      const bool persist = ((a->R == nullptr && persist_bias) || res_small_k) && a->row_map == nullptr &&
+                           a->N <= ph8::BIAS_MAX && g_use_glds != 11 && g_use_glds != 20 &&
                            (long long)a->M * a->lda * 2 < (1LL << 31) && (long long)a->N * a->ldb * 2 < (1LL << 31);
       if (persist) {
         // fast paths 12..15: persistent-kernel diagnostics (bit 0: relaxed waits after full-tile epilogues,

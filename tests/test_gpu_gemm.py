@@ -213,7 +213,7 @@ def test_gemm8_persistent(cuda, act, M, N, K, Bt, variant):
     bias = None if variant == "nobias" else torch.randn(N, generator=g).to(cuda)
     cdt = torch.float32 if variant == "f32out" else torch.bfloat16
     outs = []
-    for fast in (1, 11):
+    for fast in (23, 11):  # 23: the persistent kernel for bias / activation kinds (opt-in), 11: one tile per WG
         lib.octsam_gemm_set_fast_path(fast | 256)
         out = torch.full((Bt, M, N), float("nan"), device=cuda, dtype=cdt)
         pout = torch.zeros(Bt, M, N, device=cuda, dtype=torch.bfloat16) if variant == "pre" else None
