@@ -104,6 +104,23 @@ __device__ __forceinline__ typename ET<E>::v8 pack8(const f32x16& a, int base) {
   return r;
 }
 
+// Online softmax with a lazy reference (base-2 units): the running reference m moves only when a tile's
+// maximum exceeds it by more than LAZY, so the O / l rescale (a wave-uniform branch) runs on a handful of tiles
+// instead of almost every one. p = exp2(score - m) <= 2^LAZY then; O / l is invariant to the reference.
+constexpr float LAZY = 8.0f;
+template <int NTD>
+__device__ __forceinline__ void lazy_rescale(float mt, float& m_run, float& l_run, f32x16 (&acc_o)[NTD]) {
+  const bool grow = mt > m_run + LAZY;
+  if (__builtin_amdgcn_ballot_w64(grow)) {
+    const float m_new = grow ? mt : m_run;
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 on the first tile, 1 on lanes that keep m
+    m_run = m_new;
+    l_run *= alpha;
+#pragma unroll
+    for (int td = 0; td < NTD; ++td) acc_o[td] *= alpha;
+  }
+}
+
 // 32 table rows j0 .. j0+31 of P^T = R . Q^T for the lane's query (natural units), rows outside [0, nrows)
 // zero. R fp32 [nrows][HD], rounded to the element type like the q.k operands.
 // Split form for prologues that issue the K/V DMA after the table rows: rel_load fetches the lane's table row
@@ -411,10 +428,8 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
     for (int i = 1; i < 31; i += 2) mx = max3f(mx, sacc[i >> 4][i & 15], sacc[(i + 1) >> 4][(i + 1) & 15]);
     mx = fmaxf(mx, sacc[1][15]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, fmaf(mx, c1, rh));
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
-    const float c = rh - m_new;
+    lazy_rescale<G::NTD>(fmaf(mx, c1, rh), m_run, l_run, acc_o);
+    const float c = rh - m_run;
     f32x2 ls2 = {0.0f, 0.0f};
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2)
@@ -427,11 +442,7 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
         sacc[t2][r + 1] = pv[1];
         ls2 += pv;  // v_pk_add_f32
       }
-    l_run = fmaf(l_run, alpha, ls2[0] + ls2[1]);
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
-#pragma unroll
-      for (int td = 0; td < G::NTD; ++td) acc_o[td] *= alpha;
-    }
+    l_run += ls2[0] + ls2[1];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) pv_step<HD, E>(slot, zero, ks, pack8<E>(sacc[ks >> 1], 8 * (ks & 1)), acc_o, lane);
   }
@@ -555,14 +566,12 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
 #pragma unroll
     for (int k = 0; k < 2 * nb; ++k) mx = fmaxf(mx, fmaf(mh[k], c1, relh[4 * tile + k]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
+    lazy_rescale<G::NTD>(mx, m_run, l_run, acc_o);
     float ls = 0.0f;
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
       if (t2 >= nb) continue;
-      const float c0 = relh[4 * tile + 2 * t2] - m_new, cc1 = relh[4 * tile + 2 * t2 + 1] - m_new;
+      const float c0 = relh[4 * tile + 2 * t2] - m_run, cc1 = relh[4 * tile + 2 * t2 + 1] - m_run;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], c1, r < 8 ? c0 : cc1));
@@ -570,11 +579,7 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
         ls += pv;
       }
     }
-    l_run = fmaf(l_run, alpha, ls);
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {
-#pragma unroll
-      for (int td = 0; td < G::NTD; ++td) acc_o[td] *= alpha;
-    }
+    l_run += ls;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       if (ks >= 2 * nb) break;
