@@ -74,6 +74,9 @@ class FusedTrainStep:
         self._side = None
         self.pipeline = pipeline and graphs
         self._enc_stream = None
+        # lookahead stream priority: equal to the main stream's (measured: a high-priority lookahead 17.8 -> 21.3
+        # ms/step, the step on a high-priority stream instead 17.7 -> 18.0; scripts/prio_ab.py)
+        self.enc_priority = 0
         self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
         self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
         self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
@@ -353,7 +356,7 @@ class FusedTrainStep:
             return  # the other set is captured when a step first needs it
         main = torch.cuda.current_stream()
         if self._enc_stream is None:
-            self._enc_stream = torch.cuda.Stream(device=main.device)
+            self._enc_stream = torch.cuda.Stream(device=main.device, priority=self.enc_priority)
         enc = self._enc_stream
         enc.wait_event(es["b_done"])
         ready = torch.cuda.Event()
