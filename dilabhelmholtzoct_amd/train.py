@@ -77,6 +77,9 @@ class FusedTrainStep:
         # lookahead stream priority: equal to the main stream's (measured: a high-priority lookahead 17.8 -> 21.3
         # ms/step, the step on a high-priority stream instead 17.7 -> 18.0; scripts/prio_ab.py)
         self.enc_priority = 0
+        # encoder graph sets the lookahead cycles through (2: the encoder of step t+2 waits for the backward of
+        # step t; 3 sets measured the same, 17.72 vs 17.76 ms/step: the encoder stream is busy throughout)
+        self.pipeline_sets = 2
         self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
         self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
         self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
@@ -342,7 +345,7 @@ class FusedTrainStep:
         gb.replay()
         if self.pipeline:
             es["b_done"].record(main)
-            self._parity[ekey0] = 1 - par
+            self._parity[ekey0] = (par + 1) % self.pipeline_sets
         return st.loss_out
 
     def _launch_lookahead(self, ekey0, par, next_px):
@@ -351,7 +354,7 @@ class FusedTrainStep:
         stream. Any prompt count: only the pixel shape has to match."""
         if (tuple(next_px.shape), next_px.dtype) != ekey0:
             return  # another pixel shape: its first step runs E itself
-        es = self._esets.get(ekey0 + (1 - par,))
+        es = self._esets.get(ekey0 + ((par + 1) % self.pipeline_sets,))
         if es is None:
             return  # the other set is captured when a step first needs it
         main = torch.cuda.current_stream()

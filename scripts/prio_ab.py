@@ -21,15 +21,17 @@ model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(device)
 K = 10
 steps = {}
 hi = torch.cuda.Stream(device=device, priority=-1)
-for prio in (0, 1):
+VARS = [tuple(int(x) for x in v.split(":")) for v in os.environ.get("VARS", "2:0,3:0,3:-1").split(",")]
+for sets, eprio in VARS:
     st = FusedTrainStep(model, lr=0.0, topological=True, graphs=True, pipeline=True)
-    steps[prio] = st
+    st.pipeline_sets, st.enc_priority = sets, eprio
+    steps[(sets, eprio)] = st
 best = {}
 for rnd in range(4):
     for prio, st in steps.items():
-      with torch.cuda.stream(hi if prio == 1 else torch.cuda.default_stream(device)):
-        for i in range(3):
-            st.step(batch, next_batch=batch if i < 2 else None)
+      with torch.cuda.stream(torch.cuda.default_stream(device)):
+        for i in range(4):
+            st.step(batch, next_batch=batch if i < 3 else None)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(K):
@@ -37,5 +39,5 @@ for rnd in range(4):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / K
         best[prio] = min(best.get(prio, 1e30), ms)
-        print(f"round {rnd} variant {prio}: {ms:.3f} ms/step", flush=True)
+        print(f"round {rnd} sets:priority {prio}: {ms:.3f} ms/step", flush=True)
 print(best)
