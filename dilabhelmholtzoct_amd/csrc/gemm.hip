@@ -1792,8 +1792,10 @@ int launch_gemm8n192(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
 }
 
 // 256x192 tiles when they fill the chip's waves better than 256x256 ones (3/4 of the work per tile);
-// g_n192 = 0 (fast path 21, A/B diagnostics) keeps the 256x256 kernels
-static int g_n192 = 1;
+// 256x192 tiles are opt-in (fast path 24): standalone they fill the chip's waves better for N = 768 / 2304, but
+// under the encoder lookahead (decoder kernels share the chip, quantisation stops mattering) the 256x256 tiles'
+// fewer epilogues win, 17.77 -> 17.43 ms/step (scripts/step_ab2.py, profiles/r02g/n192_ab.log)
+static int g_n192 = 0;
 inline bool prefer_n192(const octsam_gemm_args* a, int n_cu) {
   if (a->N % 192 != 0 || a->K < 64) return false;
   const long long tm = (a->M + 255) / 256;
@@ -2140,7 +2142,7 @@ int& last_path() { static thread_local int v = 0; return v; }
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_small = (enable & 256) ? 0 : 1;
   g_use_glds = enable & 255;
-  g_n192 = g_use_glds == 21 ? 0 : 1;
+  g_n192 = g_use_glds == 24 ? 1 : 0;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
 #endif
