@@ -12,7 +12,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liboctsam_hip.so")
+# OCTSAM_LIB: another build of the same ABI (A/B diagnostics in scripts/, never set by the package itself)
+LIB_PATH = os.environ.get("OCTSAM_LIB") or os.path.join(_HERE, "liboctsam_hip.so")
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
