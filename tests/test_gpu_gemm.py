@@ -513,3 +513,18 @@ def test_fp16_encoder_pieces(cuda):
     c = torch.empty(1000, 1280, device=cuda, dtype=torch.float16)
     kernels.cast_bf16(x, c)
     assert torch.equal(c, x.to(torch.float16))
+
+
+@pytest.mark.parametrize("n", [32768 * 768, 4096 * 8 + 8, 1000 * 8, 37, 8 * 3 + 5])
+def test_cast_vectorized(cuda, n):
+    """fp32 -> bf16 / fp16 casts: the 8-per-thread kernel (n % 8 == 0, aligned) and the scalar fallback
+    (ragged n, offset views) round exactly like torch's casts, special values included."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(n % 1000)
+    x = (torch.randn(n + 1, generator=g) * 100).to(cuda)
+    x[:4] = torch.tensor([float("inf"), -0.0, 1e-40, 65519.0])
+    for dt in (torch.bfloat16, torch.float16):
+        for src in (x[:n], x[1:n + 1]):  # aligned, and 4-B offset (scalar path)
+            out = torch.empty(n, device=cuda, dtype=dt)
+            kernels.cast_bf16(src, out)
+            assert torch.equal(out, src.to(dt))
