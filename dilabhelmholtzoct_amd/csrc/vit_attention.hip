@@ -553,33 +553,37 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
     for (int t2 = 0; t2 < 2; ++t2) {
       if (t2 >= nb) continue;
       sacc[t2] = qk_block<HD, E>(slot, t2, qf, init, l32, h);
-      float a = -INFINITY, b = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 8; r += 2) {
-        a = fmaxf(a, fmaxf(sacc[t2][r], sacc[t2][r + 1]));
-        b = fmaxf(b, fmaxf(sacc[t2][r + 8], sacc[t2][r + 9]));
-      }
-      mh[2 * t2] = a;
-      mh[2 * t2 + 1] = b;
+      // three-input maxima (padding columns hold -inf, never NaN)
+      float a = max3f(sacc[t2][0], sacc[t2][1], sacc[t2][2]), b = max3f(sacc[t2][8], sacc[t2][9], sacc[t2][10]);
+      a = max3f(a, sacc[t2][3], sacc[t2][4]);
+      b = max3f(b, sacc[t2][11], sacc[t2][12]);
+      a = max3f(a, sacc[t2][5], sacc[t2][6]);
+      b = max3f(b, sacc[t2][13], sacc[t2][14]);
+      mh[2 * t2] = fmaxf(a, sacc[t2][7]);
+      mh[2 * t2 + 1] = fmaxf(b, sacc[t2][15]);
     }
     float mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 2 * nb; ++k) mx = fmaxf(mx, fmaf(mh[k], c1, relh[4 * tile + k]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     lazy_rescale<G::NTD>(mx, m_run, l_run, acc_o);
-    float ls = 0.0f;
+    f32x2 ls2 = {0.0f, 0.0f};
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) {
       if (t2 >= nb) continue;
       const float c0 = relh[4 * tile + 2 * t2] - m_run, cc1 = relh[4 * tile + 2 * t2 + 1] - m_run;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sacc[t2][r], c1, r < 8 ? c0 : cc1));
-        sacc[t2][r] = pv;
-        ls += pv;
+      for (int r = 0; r < 16; r += 2) {
+        const float cc = r < 8 ? c0 : cc1;
+        const f32x2 x = {sacc[t2][r], sacc[t2][r + 1]};
+        const f32x2 y = x * c1 + (f32x2){cc, cc};  // v_pk_fma_f32
+        const f32x2 pv = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+        sacc[t2][r] = pv[0];
+        sacc[t2][r + 1] = pv[1];
+        ls2 += pv;  // v_pk_add_f32
       }
     }
-    l_run += ls;
+    l_run += ls2[0] + ls2[1];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       if (ks >= 2 * nb) break;
