@@ -98,3 +98,44 @@ def test_data_parallel_step_matches_single_process(cuda, tmp_path):
     assert err.max().item() < 2.5e-3, err.max().item()
     assert (err > 1e-4).float().mean().item() < 0.05
     assert (ref - init.cpu()).abs().max().item() > 1e-4
+
+
+def _worker_pipe(rank, world, port, path, pipeline):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    dev = torch.device("cuda", 0)
+    _, shards = _global_batch()
+    batch = data.to_device_batch(shards[rank], dev)
+    model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(dev)
+    step = FusedTrainStep(model, topological=True, process_group=dist.group.WORLD, graphs=True, pipeline=pipeline)
+    losses = [step.step(batch, n_global=2, next_batch=batch if k < 3 else None).clone() for k in range(4)]
+    step.flush()
+    torch.cuda.synchronize()
+    torch.save({"flat": model.mask_decoder.flat.detach().cpu(), "losses": torch.stack(losses).cpu()},
+               f"{path}.{int(pipeline)}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_with_encoder_lookahead(cuda, tmp_path):
+    """The encoder lookahead under data parallelism (deferred Adam, side-stream all-reduce, the next encoder
+    queued before the deferred update): losses and parameters bit-identical to the DP step without it."""
+    path = str(tmp_path / "pipe")
+    ctx = mp.get_context("spawn")
+    for pipeline in (False, True):
+        port = _port()
+        procs = [ctx.Process(target=_worker_pipe, args=(r, 2, port, path, pipeline)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0, p.exitcode
+    for rank in range(2):
+        a = torch.load(f"{path}.0.{rank}", weights_only=True)
+        b = torch.load(f"{path}.1.{rank}", weights_only=True)
+        assert torch.equal(a["losses"], b["losses"])
+        assert torch.equal(a["flat"], b["flat"])
