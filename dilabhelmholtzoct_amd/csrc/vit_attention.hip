@@ -59,6 +59,16 @@ constexpr int NW = 8, THR = NW * 64, NBUF = 3;
 constexpr float L2E = 1.4426950408889634f;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float max3f(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
+// The two lane halves hold one query's statistics: v_permlane32_swap of x with itself gives every lane {x of the
+// lower half, x of the upper half} (lane i and lane i ^ 32 see the same pair), so max / sum across the halves
+// take one swap and one VALU op (no ds_bpermute round trip on the softmax's dependency chain)
+__device__ __forceinline__ f32x2 halves(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return (f32x2){__builtin_bit_cast(float, (uint32_t)r[0]), __builtin_bit_cast(float, (uint32_t)r[1])};
+}
+__device__ __forceinline__ float max_halves(float x) { const f32x2 h = halves(x); return fmaxf(h[0], h[1]); }
+__device__ __forceinline__ float sum_halves(float x) { const f32x2 h = halves(x); return h[0] + h[1]; }
 
 template <int HD> struct Geo {
   static_assert(HD == 64 || HD == 80, "head_dim 64 or 80");
@@ -427,7 +437,7 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
 #pragma unroll
     for (int i = 1; i < 31; i += 2) mx = max3f(mx, sacc[i >> 4][i & 15], sacc[(i + 1) >> 4][(i + 1) & 15]);
     mx = fmaxf(mx, sacc[1][15]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_halves(mx);
     lazy_rescale<G::NTD>(fmaf(mx, c1, rh), m_run, l_run, acc_o);
     const float c = rh - m_run;
     f32x2 ls2 = {0.0f, 0.0f};
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) pv_step<HD, E>(slot, zero, ks, pack8<E>(sacc[ks >> 1], 8 * (ks & 1)), acc_o, lane);
   }
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = sum_halves(l_run);
   store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
@@ -565,7 +575,7 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
     float mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 2 * nb; ++k) mx = fmaxf(mx, fmaf(mh[k], c1, relh[4 * tile + k]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_halves(mx);
     lazy_rescale<G::NTD>(mx, m_run, l_run, acc_o);
     f32x2 ls2 = {0.0f, 0.0f};
 #pragma unroll
@@ -591,7 +601,7 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
     }
   }
   if (!qvalid) return;
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = sum_halves(l_run);
   const long long orow = grid == 0 ? (long long)win * T + q : wr.row(q);
   store_out<HD, E>(out + orow * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
