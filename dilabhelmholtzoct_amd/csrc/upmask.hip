@@ -20,6 +20,33 @@
 #include "../../include/octsam.h"
 
 namespace {
+// The value of lane ^ 32 (lane ^ 16): v_permlane32_swap (v_permlane16_swap) of x with itself leaves every lane
+// {x of the lower, x of the upper} lane of its pair; pick the partner's by the lane's own half (hi = lane bit 5
+// (bit 4)). One swap and one select instead of a ds_bpermute round trip inside the VALU-bound loop.
+__device__ __forceinline__ float xor32_value(float x, bool hi) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (uint32_t)(hi ? r[0] : r[1]));
+}
+// Sum over the 16 lanes of a row (every lane gets it): DPP quad swaps (xor 1, xor 2) then row rotations by 4 and 8
+// — no LDS traffic. Fixed order, so the reduction is deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x124>(v);  // row_ror:4
+  v += dpp_mov<0x128>(v);  // row_ror:8
+  return v;
+}
+__device__ __forceinline__ float xor16_value(float x, bool hi) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (uint32_t)(hi ? r[0] : r[1]));
+}
+
 namespace um {
 constexpr int ROWS = 128;               // up1 rows per tile
 constexpr int TILES_PER_P = 16384 / ROWS;
@@ -156,10 +183,10 @@ __global__ __launch_bounds__(256, 3) void upmask_fwd_kernel(const bf16* __restri
         const bool hi2 = g & 2, hi1 = g & 1;
         float a0 = hi2 ? m[t][2] : m[t][0], a1 = hi2 ? m[t][3] : m[t][1];
         const float s0 = hi2 ? m[t][0] : m[t][2], s1 = hi2 ? m[t][1] : m[t][3];
-        a0 += __shfl_xor(s0, 32, 64);
-        a1 += __shfl_xor(s1, 32, 64);
+        a0 += xor32_value(s0, hi2);
+        a1 += xor32_value(s1, hi2);
         float k = hi1 ? a1 : a0;
-        k += __shfl_xor(hi1 ? a0 : a1, 16, 64);
+        k += xor16_value(hi1 ? a0 : a1, hi1);
         sm[t * 512 + pix_local(rr, g)] = k;
       }
     }
@@ -368,8 +395,7 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float v = hacc[t][hh][i];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+          v = row16_sum(v);
           if (c == 0) s_red[w * NS * 32 + t * 32 + 16 * hh + 4 * g + i] = v;
         }
     __syncthreads();  // (C) dpre tile and d hyper rows complete
@@ -415,8 +441,7 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float v = bacc[hh][i];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+      v = row16_sum(v);
       if (c == 0) s_red[w * 32 + 16 * hh + 4 * g + i] = v;
     }
   __syncthreads();
