@@ -92,11 +92,42 @@ __device__ __forceinline__ void stv(void* base, long long idx, int ty, const flo
   }
 }
 
+// Cross-lane sums without LDS round trips: DPP within a row of 16 lanes, v_permlane16/32_swap across rows.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// x + (x of lane ^ 16) / (x of lane ^ 32): the swap of x with itself leaves each lane {lower, upper} of its pair
+__device__ __forceinline__ float add_xor16(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (uint32_t)r[0]) + __builtin_bit_cast(float, (uint32_t)r[1]);
+}
+__device__ __forceinline__ float add_xor32(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (uint32_t)r[0]) + __builtin_bit_cast(float, (uint32_t)r[1]);
+}
+
+// sum over each aligned group of G lanes, in every lane of the group (fixed order: deterministic)
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if constexpr (G >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  if constexpr (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: the other quad of the 8 (all hold quad sums)
+  if constexpr (G >= 16) v += dpp_mov<0x140>(v); // row_mirror: the other 8 of the row (all hold 8-lane sums)
+  if constexpr (G >= 32) v = add_xor16(v);
+  if constexpr (G >= 64) v = add_xor32(v);
   return v;
+}
+
+// v + (v of lane ^ O) for a single lane distance O >= 8 (lane positions matter: per-column partials)
+template <int O>
+__device__ __forceinline__ float add_lane_xor(float v) {
+  static_assert(O == 8 || O == 16 || O == 32, "lane distance 8, 16 or 32");
+  if constexpr (O == 8) return v + dpp_mov<0x128>(v);  // row_ror:8 = lane ^ 8 within the row
+  else if constexpr (O == 16) return add_xor16(v);
+  else return add_xor32(v);
 }
 
 template <int D>
@@ -227,10 +258,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
   // rows of one wave that share columns: fold the RPW groups, then the 4 waves through LDS
 #pragma unroll
   for (int e = 0; e < PL; ++e) {
-#pragma unroll
-    for (int o = G; o < 64; o <<= 1) {
-      dwa[e] += __shfl_xor(dwa[e], o, 64);
-      dba[e] += __shfl_xor(dba[e], o, 64);
+    if constexpr (G <= 8) {
+      dwa[e] = add_lane_xor<8>(dwa[e]);
+      dba[e] = add_lane_xor<8>(dba[e]);
+    }
+    if constexpr (G <= 16) {
+      dwa[e] = add_lane_xor<16>(dwa[e]);
+      dba[e] = add_lane_xor<16>(dba[e]);
+    }
+    if constexpr (G <= 32) {
+      dwa[e] = add_lane_xor<32>(dwa[e]);
+      dba[e] = add_lane_xor<32>(dba[e]);
     }
   }
   __shared__ float red[2][4][D];
