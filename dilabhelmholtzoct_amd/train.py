@@ -284,21 +284,30 @@ class FusedTrainStep:
 
     @staticmethod
     def _src_tag(t):
-        return None if t is None else (t.data_ptr(), t._version, t.device)
+        """Identity of an input as last copied: the tensor itself (held, so its storage cannot be handed to a
+        later batch while the tag lives — a (data_ptr, version) tag matched a new batch that the caching
+        allocator placed at a freed batch's address) and its version counter (in-place writes)."""
+        return None if t is None else (t, t._version)
+
+    @staticmethod
+    def _same(a, b):
+        if a is None or b is None:
+            return a is None and b is None
+        return a[0] is b[0] and a[1] == b[1]
 
     def _copy_in(self, g, inputs):
         """Copy a new batch into the captured graphs' static inputs (skipped for the tensors that were copied
         last and have not changed since: same storage, same version counter)."""
         tags = tuple(self._src_tag(t) for t in inputs)
         for dst, src, tag, old in zip(g["static"], inputs, tags, g["src"]):
-            if dst is not None and src is not None and tag != old:
+            if dst is not None and src is not None and not self._same(tag, old):
                 dst.copy_(src, non_blocking=True)
         g["src"] = tags
 
     @staticmethod
     def _pixel_in(es, px):
         tag = FusedTrainStep._src_tag(px)
-        if tag != es["src"]:
+        if not FusedTrainStep._same(tag, es["src"]):
             es["pixel"].copy_(px, non_blocking=True)
             es["src"] = tag
 
@@ -319,7 +328,7 @@ class FusedTrainStep:
         main = torch.cuda.current_stream()
         pre = self._prefetch
         self._prefetch = None
-        if pre is not None and pre[0] is es and pre[1] == self._src_tag(pixel_values):
+        if pre is not None and pre[0] is es and self._same(pre[1], self._src_tag(pixel_values)):
             main.wait_event(es["e_done"])  # this batch's E ran ahead on the encoder stream
         else:
             if pre is not None:

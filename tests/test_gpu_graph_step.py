@@ -67,3 +67,36 @@ def test_graph_step_new_batches_match_eager(cuda):
         assert torch.equal(a, b), (a, b)
     assert torch.equal(fe, fg)
     assert 1 <= ng <= 3
+
+
+def test_graph_step_batch_in_reused_storage(cuda):
+    """A new batch placed by the caching allocator in the storage of a freed earlier batch (same addresses,
+    version counters 0): the graphs' copy-in must still happen (the input tags hold the tensors, not their
+    addresses). Losses and parameters bit-identical to eager."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+
+    def batch(epoch):
+        sd = data.SAMDataset(data.synthetic_oct(seed=3, n=2), {"prompt_type": "bboxes"}, epoch_seed=epoch)
+        b = data.custom_collate([sd[i] for i in range(2)])
+        return data.to_device_batch(data.process_batch(data.make_processor(), b, "bboxes"), cuda)
+
+    runs = []
+    for graphs in (False, True):
+        model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(cuda)
+        step = FusedTrainStep(model, topological=True, graphs=graphs)
+        losses, ptrs = [], []
+        for epoch in (0, 1, 2, 1):
+            b = batch(epoch)
+            ptrs.append(b["input_boxes"].data_ptr())
+            losses.append(step.step(b).clone())
+            del b
+        step.flush()
+        torch.cuda.synchronize()
+        runs.append((losses, model.mask_decoder.flat.detach().clone(), ptrs))
+    (le, fe, _), (lg, fg, ptrs) = runs
+    for a, b in zip(le, lg):
+        assert torch.equal(a, b), (a, b)
+    assert torch.equal(fe, fg)
+    print("input_boxes storage reused:", len(set(ptrs)) < len(ptrs))
