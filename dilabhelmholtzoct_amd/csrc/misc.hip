@@ -105,7 +105,19 @@ __global__ __launch_bounds__(256) void group_sum8_kernel(const bf16* __restrict_
   const bf16* src = in + ((long long)g * nper * rows_per + r) * ld_in + c;
   const long long step = (long long)rows_per * ld_in;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j = 0; j < nper; ++j) {
+  // 8 loads in flight per thread (the sum stays in j order: same bits as one load at a time); the group count is
+  // small (few waves per CU), so each thread needs its own memory-level parallelism
+  int j = 0;
+  for (; j + 8 <= nper; j += 8) {
+    bf16x8 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *(const bf16x8*)(src + (j + u) * step);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += (float)v[u][k];
+  }
+  for (; j < nper; ++j) {
     const bf16x8 v = *(const bf16x8*)(src + j * step);
 #pragma unroll
     for (int k = 0; k < 8; ++k) s[k] += (float)v[k];

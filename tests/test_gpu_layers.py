@@ -193,14 +193,21 @@ def test_patchify_bf16(cuda):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("ld,cols,off", [(256, 128, 0), (256, 128, 128), (128, 128, 0), (24, 12, 0)])
-def test_group_sum(cuda, ld, cols, off):
-    """out[g] = sum over the nper prompt blocks of image g (fixed order), strided column window; bf16 out."""
+@pytest.mark.parametrize("ld,cols,off,nper", [(256, 128, 0, 5), (256, 128, 128, 5), (128, 128, 0, 5), (24, 12, 0, 5),
+                                             (256, 256, 0, 21), (256, 128, 128, 16)])
+def test_group_sum(cuda, ld, cols, off, nper):
+    """out[g] = sum over the nper prompt blocks of image g (fixed order), strided column window; bf16 out. The
+    8-column kernel keeps 8 loads in flight but adds in block order: bit-identical to a sequential fp32 sum."""
     from dilabhelmholtzoct_amd import kernels
-    g = torch.Generator().manual_seed(ld + cols + off)
-    G, nper, rows = 3, 5, 4096
+    g = torch.Generator().manual_seed(ld + cols + off + nper)
+    G, rows = 3, 4096
     x = torch.randn(G * nper * rows, ld, generator=g).to(cuda, torch.bfloat16)
     out = torch.empty(G * rows, cols, device=cuda, dtype=torch.bfloat16)
     kernels.group_sum(x[:, off:], out, ld_in=ld, cols=cols, groups=G, nper=nper, rows_per=rows)
     ref = x[:, off:off + cols].float().view(G, nper, rows, cols).sum(1).reshape(G * rows, cols)
     assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    blocks = x[:, off:off + cols].float().view(G, nper, rows, cols)
+    seq = blocks[:, 0].clone()
+    for j in range(1, nper):
+        seq += blocks[:, j]
+    assert torch.equal(out, seq.reshape(G * rows, cols).to(torch.bfloat16))
