@@ -211,3 +211,20 @@ def test_group_sum(cuda, ld, cols, off, nper):
     for j in range(1, nper):
         seq += blocks[:, j]
     assert torch.equal(out, seq.reshape(G * rows, cols).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("rows,cols,dt", [(688128, 256, torch.bfloat16), (4097, 256, torch.float32),
+                                          (1176, 64, torch.bfloat16), (33, 128, torch.float32)])
+def test_colsum(cuda, rows, cols, dt):
+    """Column sums (bias gradients) over many rows: fixed-order partials (deterministic), against torch fp64."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(rows + cols)
+    x = torch.randn(rows, cols, generator=g).to(cuda, dt)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(cols, device=cuda)
+        kernels.colsum(x, rows, cols, out)
+        outs.append(out)
+    ref = x.double().sum(0)
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0].double() - ref).abs().max().item() < 1e-4 * max(1.0, rows ** 0.5)
