@@ -490,6 +490,18 @@ def main():
     step.flush()  # a deferred (overlapped) update belongs to the timed work
     barrier()
     dt = time.perf_counter() - t0
+    # the same graphs without the lookahead hint (each step runs its own encoder in line): the sequential rate
+    seq_ms = None
+    if pipe:
+        nseq = max(3, args.steps // 2)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(nseq):
+            step.step(batch)
+        step.flush()
+        barrier()
+        seq_ms = (time.perf_counter() - t1) * 1e3 / nseq
+        log(f"rank {rank}: sequential (no lookahead) {seq_ms:.2f} ms/step")
     # Roofline of the dominant kernel: HIP events around each of its launches. Graph replays run no
     # Python, so the launches are timed in `roof_steps` eager steps of the same batch right after the
     # timed region (same kernels, shapes and stream); rocprofv3 over the graph run must agree. The same
@@ -621,6 +633,7 @@ def main():
                        "exec": "eager" if args.eager else
                        ("hipgraph + encoder lookahead (next step's frozen encoder on a side stream during this "
                         "step's decoder; each timed step runs its own encoder)" if pipe else "hipgraph")},
+            "sequential_ms_per_step": None if seq_ms is None else round(seq_ms, 3),
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
             "val_dice": val_dice,
             "val_metrics_mean": val_metrics,
