@@ -14,7 +14,25 @@
 #include "common.h"
 #include "../../include/octsam.h"
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 namespace {
+// Symmetric cross-lane reductions between lane and lane ^ 16 / lane ^ 32 by v_permlane16/32_swap of x with itself
+// (each lane ends with {lower, upper} of its pair) instead of a ds_bpermute round trip.
+__device__ __forceinline__ f32x2_t pair16(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return {__builtin_bit_cast(float, (uint32_t)r[0]), __builtin_bit_cast(float, (uint32_t)r[1])};
+}
+__device__ __forceinline__ f32x2_t pair32(float x) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return {__builtin_bit_cast(float, (uint32_t)r[0]), __builtin_bit_cast(float, (uint32_t)r[1])};
+}
+__device__ __forceinline__ float max_xor16(float x) { const f32x2_t p = pair16(x); return fmaxf(p[0], p[1]); }
+__device__ __forceinline__ float max_xor32(float x) { const f32x2_t p = pair32(x); return fmaxf(p[0], p[1]); }
+__device__ __forceinline__ float add_xor16(float x) { const f32x2_t p = pair16(x); return p[0] + p[1]; }
+__device__ __forceinline__ float add_xor32(float x) { const f32x2_t p = pair32(x); return p[0] + p[1]; }
+
 
 constexpr int MAXT = 8;
 
@@ -247,8 +265,8 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
     }
     float mx = fmaxf(fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3])),
                      fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor16(mx);
+    mx = max_xor32(mx);
     const float mn = fmaxf(m, mx);
     const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
@@ -266,8 +284,8 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
     o0 = mfma32(cat8(tr_op(vimg, 0, 0, true, lane), tr_op(vimg, 1, 0, true, lane)), pf, o0);
     o1 = mfma32(cat8(tr_op(vimg, 0, 1, true, lane), tr_op(vimg, 1, 1, true, lane)), pf, o1);
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = add_xor16(l);
+  l = add_xor32(l);
   float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * PART;
   const int c = lane & 15;
   *(f32x4*)(w + c * 16 + 4 * (lane >> 4)) = c < 8 ? o0 : o1;  // O^T[d = 4g+i][n = c] -> O[n][d]
@@ -446,7 +464,7 @@ __global__ __launch_bounds__(256) void i2t_fwd_kernel(const bf16* __restrict__ q
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, s[i]) : mx;
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = max_xor16(mx);
     f32x4 e;
     float sum = 0.0f;
 #pragma unroll
@@ -454,7 +472,7 @@ __global__ __launch_bounds__(256) void i2t_fwd_kernel(const bf16* __restrict__ q
       e[i] = nv[i] ? __builtin_amdgcn_exp2f(s[i] - mx) : 0.0f;
       sum += e[i];
     }
-    sum += __shfl_xor(sum, 16, 64);
+    sum = add_xor16(sum);
     e *= 1.0f / sum;
     const s16x4 pb = pack4(e);
 #pragma unroll
@@ -514,7 +532,7 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
       float mx = -INFINITY;
 #pragma unroll
       for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, sT[i]) : mx;
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = max_xor16(mx);
       f32x4 pT;
       float sum = 0.0f;
 #pragma unroll
@@ -522,7 +540,7 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
         pT[i] = nv[i] ? __builtin_amdgcn_exp2f(sT[i] - mx) : 0.0f;
         sum += pT[i];
       }
-      sum += __shfl_xor(sum, 16, 64);
+      sum = add_xor16(sum);
       const float inv = 1.0f / sum;
       float del = 0.0f;
 #pragma unroll
@@ -530,7 +548,7 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
         pT[i] *= inv;
         del = fmaf(pT[i], dpT[i], del);
       }
-      del += __shfl_xor(del, 16, 64);
+      del = add_xor16(del);
       f32x4 dsT;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dsT[i] = pT[i] * (dpT[i] - del);
