@@ -117,6 +117,10 @@ _SIGNATURES = {
     "octsam_topo_host": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                    c_int32, c_int32, ctypes.c_double, ctypes.c_double, c_int32, c_void_p,
                                    c_void_p]),
+    "octsam_topo_w2_workspace": (c_int64, [c_int32, c_int32]),
+    "octsam_topo_w2": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                 c_void_p, c_int32, c_int32, ctypes.c_double, ctypes.c_double, c_int32, c_void_p,
+                                 c_int64, c_void_p, c_void_p, c_void_p]),
     "octsam_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, ctypes.c_double, ctypes.c_double, c_float,
                               c_float, c_float, c_float, c_void_p, c_void_p]),
 }

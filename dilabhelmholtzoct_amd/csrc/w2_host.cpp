@@ -194,9 +194,11 @@ extern "C" int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const 
     double s = 0.0;
     for (double c : costs) s += c;  // Python sum() over floats, left to right
     const double tot = (double)(float)s;
-    total += std::pow(tot, 1.0 / q);
+    // q = 2 (the call site): the 1/q power as a correctly rounded sqrt, as octsam_topo_w2 computes it on the device
+    total += q == 2.0 ? std::sqrt(tot) : std::pow(tot, 1.0 / q);
     if (want_grad) {
-      const double dd = tot > 0 ? (1.0 / q) * std::pow(tot, 1.0 / q - 1.0) : std::numeric_limits<double>::infinity();
+      const double dd = tot > 0 ? (q == 2.0 ? 0.5 / std::sqrt(tot) : (1.0 / q) * std::pow(tot, 1.0 / q - 1.0))
+                                : std::numeric_limits<double>::infinity();
       // numpy 2 (NEP 50): python-float scale * float32 gradient is computed in float32
       const float scale = (float)(lamda / n_entries * dd);
       for (int t = e0; t < e1; ++t) {

@@ -62,10 +62,27 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         pre_f32=int(pre_out is not None and pre_out.dtype == torch.float32),
         conv_c=conv_c, a2_rows=a2_rows, b2_rows=b2_rows, a_blk=a_remap[0], a_rep=a_remap[1],
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
-        c_rows=min(out.numel() // ldc, 2 ** 31 - 1) if row_map is not None else 0,
+        c_rows=_mapped_rows(out, ldc, residual, ldr, pre_out) if row_map is not None else 0,
         a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
+
+
+def _span_rows(t: torch.Tensor, ld: int) -> int:
+    """Rows of leading dimension ld addressable from t's first element to the end of its storage (a column-sliced
+    or offset view included)."""
+    return (t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()) // ld
+
+
+def _mapped_rows(out, ldc, residual, ldr, pre_out) -> int:
+    """c_rows of a row-mapped GEMM: the rows every row-mapped operand (C, R, C_pre) can hold; the lean epilogue
+    range-checks C, R and C_pre against c_rows * ld."""
+    rows = _span_rows(out, ldc)
+    if residual is not None:
+        rows = min(rows, _span_rows(residual, ldr))
+    if pre_out is not None:
+        rows = min(rows, _span_rows(pre_out, ldc))
+    return min(rows, 2 ** 31 - 1)
 
 
 def splitk_reduce(partials: torch.Tensor, out: torch.Tensor, splits: int, beta: float = 0.0) -> torch.Tensor:

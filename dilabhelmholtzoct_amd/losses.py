@@ -13,6 +13,7 @@ The fused training step (train.py) calls the same kernels directly without autog
 from __future__ import annotations
 
 import functools
+import math
 
 import numpy as np
 import torch
@@ -251,6 +252,9 @@ def topo_device_forward(masks: torch.Tensor, gt_u8: torch.Tensor, midx: torch.Te
               K.ptr(both[:Kn]), K.ptr(both[Kn:]))
     p0, p1, ess, cnt = K.cubical_ph(both, max_pairs=max_pairs)
     if feat_d == 0:
+        # one more row for the essential pair: a map whose finite H0 pairs fill max_pairs (count saturated at
+        # max_pairs) must not scatter past the buffer
+        p0 = torch.cat([p0, torch.zeros((2 * Kn, 1, 2), dtype=p0.dtype, device=dev)], 1)
         rows = torch.arange(2 * Kn, device=dev)
         p0[rows, cnt[:, 0].long()] = ess
         cnt = cnt.clone()
@@ -266,6 +270,51 @@ def _entry_csr(entries, maps):
     off = np.zeros(len(entries) + 1, dtype=np.int32)
     off[1:] = np.cumsum([len(e) for e in entries])
     return flat, off
+
+
+@functools.lru_cache(maxsize=64)
+def _entry_tables(entries, maps):
+    """_entry_csr plus map_entry [Kn]: the loss entry holding each map position (-1 = none)."""
+    flat, off = _entry_csr(entries, maps)
+    pos = {m: i for i, m in enumerate(maps)}
+    map_entry = np.full(len(maps), -1, np.int32)
+    for e, ms in enumerate(entries):
+        for m in ms:
+            map_entry[pos[m]] = e
+    return flat, off, map_entry
+
+
+_DEV_ENTRY: dict = {}
+
+
+def _entry_tables_device(entries, maps, device):
+    """Device copies of _entry_tables (cached: fixed addresses, so captured graphs may read them)."""
+    key = (tuple(tuple(e) for e in entries), tuple(maps), str(device))
+    if key not in _DEV_ENTRY:
+        _DEV_ENTRY[key] = tuple(torch.from_numpy(a).to(device) for a in _entry_tables(key[0], key[1]))
+    return _DEV_ENTRY[key]
+
+
+def topo_w2_device(pairs: torch.Tensor, cnt: torch.Tensor, vals: torch.Tensor, entries, maps, *, lamda=0.1,
+                   feat_d=1, loss_q=2, want_grad=True):
+    """Device half of topo_loss's forward and backward (topological_loss.py:68-96): the exact
+    W_q transport per map on the GPU (octsam_topo_w2, bit-identical to octsam_topo_host at q = 2), the loss and
+    d loss / d pred-map values — no host sync, capturable. pairs / cnt / vals as topo_device_forward returns
+    them. Returns (loss float64 [1] device, dpred fp32 [Kn, nvals] device or None); the loss is NaN if a pair
+    count exceeded max_pairs (impossible at the default kernels.ph_max_pairs)."""
+    Kn = len(maps)
+    dev = pairs.device
+    mp, nvals = int(pairs.shape[1]), int(vals.shape[1])
+    flat, off, map_entry = _entry_tables_device(entries, maps, dev)
+    lib = _lib.load()
+    ws_bytes = int(lib.octsam_topo_w2_workspace(Kn, mp))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    loss = torch.empty(1, dtype=torch.float64, device=dev)
+    dpred = torch.empty((Kn, nvals), dtype=torch.float32, device=dev) if want_grad else None
+    _lib.call("octsam_topo_w2", K.ptr(pairs), K.ptr(cnt), K.ptr(vals), Kn, mp, nvals, K.ptr(flat), K.ptr(off),
+              K.ptr(map_entry), len(entries), 0 if feat_d == 0 else 1, float(loss_q), float(lamda), int(want_grad),
+              K.ptr(ws), ws_bytes, K.ptr(loss), K.ptr(dpred))
+    return loss, dpred
 
 
 def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entries, maps, *, lamda=0.1, feat_d=1,
@@ -325,24 +374,38 @@ def total_persistence_host(pairs_h, cnt_h, vals_h, entries, maps, *, col, q, lam
 
 def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch.Tensor | None, *, lamda=0.1,
                           interp=50, feat_d=1, loss_q=2, mode="first", max_pairs=None, logits=True,
-                          global_batch: int | None = None, loss_r=False):
-    """Topological loss value (float) and, when dmask is given, its gradient added into dmask.
-    masks fp32 [B,N,H,W] (logits; sigmoid applied inside like training_utils.py:64). feat_d = 2 (the
-    reference's default) selects no pairs of a 2-D map: the loss is 0, as gudhi reports no H2 there."""
+                          global_batch: int | None = None, loss_r=False, as_tensor=False):
+    """Topological loss value (float; as_tensor: a float64 [1] device tensor, no host sync) and, when dmask is
+    given, its gradient added into dmask. masks fp32 [B,N,H,W] (logits; sigmoid applied inside like
+    training_utils.py:64). feat_d = 2 (the reference's default) selects no pairs of a 2-D map: the loss is 0, as
+    gudhi reports no H2 there. The transport runs on the device (octsam_topo_w2); loss_r (total persistence,
+    off the reference's path) adds a host pass."""
+    zero = (lambda: torch.zeros(1, dtype=torch.float64, device=masks.device)) if as_tensor else (lambda: 0.0)
     if lamda == 0.0:
-        return 0.0
+        return zero()
     if not 0 <= feat_d <= 2:
         raise NotImplementedError("feat_d outside [0, 2] (unfiltered dimensions) is not supported")
     if feat_d == 2:
-        return 0.0
+        return zero()
     B, N, H, W = masks.shape
     if not interp and (H * W > 4096 or (H + 1) * (W + 1) + H * W > 8192):
         raise NotImplementedError(f"interp=0 needs maps the persistence kernel accepts (<= 64x63), got {H}x{W}")
     entries, maps, midx = topo_index(B, N, mode, global_batch, masks.device)
     if not entries:
-        return 0.0
+        return zero()
     pairs, cnt, both = topo_device_forward(masks, gt_u8, midx, interp=interp, feat_d=feat_d, max_pairs=max_pairs,
                                            logits=logits)
+    if not loss_r:
+        loss, dpred = topo_w2_device(pairs, cnt, both, entries, maps, lamda=lamda, feat_d=feat_d, loss_q=loss_q,
+                                     want_grad=dmask is not None)
+        if dmask is not None:
+            topo_device_backward(masks, midx, dpred, dmask, interp=interp, logits=logits)
+        if as_tensor:
+            return loss
+        v = float(loss.cpu()[0])
+        if math.isnan(v):
+            raise RuntimeError("persistence pair buffer overflow: max_pairs below kernels.ph_max_pairs(interp, interp)")
+        return v
     host = [t.cpu() for t in (pairs, cnt, both)]  # one D2H sync per step (diagrams are tiny)
     ph, ch, vh = (t.numpy() for t in host)
     loss, dpred = topo_host(ph, ch, vh, entries, maps, lamda=lamda, feat_d=feat_d, loss_q=loss_q,
@@ -353,7 +416,7 @@ def topo_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dmask: torch
     if dmask is not None:
         topo_device_backward(masks, midx, torch.from_numpy(dpred).to(masks.device), dmask, interp=interp,
                              logits=logits)
-    return loss
+    return torch.tensor([loss], dtype=torch.float64, device=masks.device) if as_tensor else loss
 
 
 class _TopoFn(torch.autograd.Function):
@@ -362,10 +425,10 @@ class _TopoFn(torch.autograd.Function):
         x = maps.float().contiguous()
         dmask = torch.zeros_like(x)
         loss = topo_forward_backward(x, gt_u8, dmask, lamda=lamda, interp=interp, feat_d=feat_d, loss_q=loss_q,
-                                     mode=mode, logits=logits, loss_r=loss_r)
+                                     mode=mode, logits=logits, loss_r=loss_r, as_tensor=True)
         ctx.save_for_backward(dmask)
         ctx.in_dtype = maps.dtype
-        return torch.tensor(loss, device=x.device, dtype=torch.float32)
+        return loss.to(torch.float32).reshape(())
 
     @staticmethod
     def backward(ctx, g):

@@ -113,9 +113,10 @@ class EvalAccumulator:
         self.C = num_classes
         self.keep_scores = keep_scores
         self.counts = [[] for _ in range(num_classes)]  # per class: list of (tp, fp, fn, tn)
-        self.scores = [[] for _ in range(num_classes)]  # per class: list of (logits row, gt row) on the device
+        self.scores = [[] for _ in range(num_classes)]  # per class: list of (logits row, gt row), host memory
         self.samples = [[] for _ in range(num_classes)]  # per class: image index of each sample (:134)
         self.n_images = 0
+        self.device = torch.device("cpu")
 
     def add(self, masks: torch.Tensor, gt_u8: torch.Tensor, mask_values, image_index=None):
         B, N = masks.shape[:2]
@@ -125,9 +126,10 @@ class EvalAccumulator:
             v = int(mv[b, c])
             self.counts[v].append(tuple(int(t) for t in conf[b, c]))
             self.samples[v].append(self.n_images + b if image_index is None else image_index[b])
-            if self.keep_scores:
-                self.scores[v].append((masks[b, c].float().clone(), gt_u8[b, c].clone()))
+            if self.keep_scores:  # host memory, as the reference keeps its arrays (HBM stays free)
+                self.scores[v].append((masks[b, c].float().cpu(), gt_u8[b, c].cpu()))
         self.n_images += B
+        self.device = masks.device
 
     def pooled_confusion(self) -> torch.Tensor:
         """int64 [C, 4] pooled (tp, fp, fn, tn) per class."""
@@ -152,11 +154,14 @@ class EvalAccumulator:
             per = [confusion_metrics(*c) for c in self.counts[v]]
             for k in per[0]:
                 smp[k][v] = float(np.mean([p[k] for p in per]))
-            if self.keep_scores:
-                xs = torch.cat([x.reshape(-1) for x, _ in self.scores[v]])
-                ys = torch.cat([y.reshape(-1) for _, y in self.scores[v]])
+            if self.keep_scores:  # one class's scores on the device at a time
+                dev = self.device
+                xs = torch.cat([x.reshape(-1) for x, _ in self.scores[v]]).to(dev)
+                ys = torch.cat([y.reshape(-1) for _, y in self.scores[v]]).to(dev)
                 cat["ap"][v] = average_precision(torch.sigmoid(xs), ys)
-                smp["ap"][v] = float(np.mean([average_precision(torch.sigmoid(x), y) for x, y in self.scores[v]]))
+                del xs, ys
+                smp["ap"][v] = float(np.mean([average_precision(torch.sigmoid(x.to(dev)), y.to(dev))
+                                              for x, y in self.scores[v]]))
         mean = {k: float(np.mean(cat[k])) for k in METRICS}
         smean = {k: float(np.mean(smp[k])) for k in METRICS}
         return {"category": cat, "sample": smp, "mean": mean, "sample_mean": smean}

@@ -22,7 +22,7 @@ import torch
 
 from . import kernels as K
 from .losses import (dicece_forward_backward, postproc_backward, postproc_forward, topo_device_backward,
-                     topo_device_forward, topo_host, topo_index)
+                     topo_device_forward, topo_host, topo_index, topo_w2_device)
 from .model import SamModel
 
 
@@ -57,8 +57,13 @@ class FusedTrainStep:
     def __init__(self, model: SamModel, lr: float = 1e-3, weight_decay: float = 0.0, topological: bool = False,
                  lamda: float = 0.1, interp: int = 50, betas=(0.9, 0.999), eps: float = 1e-8,
                  topo_mode: str = "first", process_group=None, graphs: bool = False, overlap: bool = True,
-                 pipeline: bool = False):
+                 pipeline: bool = False, w2: str = "device"):
         self.model = model
+        if w2 not in ("device", "host"):
+            raise ValueError(f"w2 must be 'device' or 'host', got {w2!r}")
+        # "device": the diagrams' transport, the topo loss and its gradient on the GPU (octsam_topo_w2): no host
+        # round trip inside the step; "host": octsam_topo_host between the forward and backward graphs (A/B)
+        self.w2 = w2
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.topological, self.lamda, self.interp, self.topo_mode = topological, lamda, interp, topo_mode
         dec = model.mask_decoder
@@ -115,7 +120,10 @@ class FusedTrainStep:
             if entries:
                 pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
                 st.topo_dev = (entries, maps, midx)
-                if st.pinned is not None:  # graph mode: async copies into fixed pinned buffers
+                if self.w2 == "device":
+                    st.topo_loss_dev, st.dp = topo_w2_device(pairs, cnt, vals, entries, maps, lamda=self.lamda,
+                                                             feat_d=1, loss_q=2, want_grad=backward)
+                elif st.pinned is not None:  # graph mode: async copies into fixed pinned buffers
                     for h, d in zip(st.pinned, (pairs, cnt, vals)):
                         h.copy_(d, non_blocking=True)
                 else:
@@ -128,8 +136,9 @@ class FusedTrainStep:
         st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
 
     def _topo_host(self, st, backward):
-        """-> topo loss (float); in backward mode also fills the device (eager) / pinned (graph) gradient."""
-        if st.topo_dev is None:
+        """-> topo loss (float); in backward mode also fills the device (eager) / pinned (graph) gradient.
+        w2 = "device": nothing to do on the host (the loss and gradient were formed in F)."""
+        if st.topo_dev is None or self.w2 == "device":
             return 0.0
         entries, maps, midx = st.topo_dev
         if st.pinned is not None:
@@ -149,14 +158,19 @@ class FusedTrainStep:
         B, N, H, W = st.masks.shape
         if backward:
             if st.topo_dev is not None:
-                if st.pinned is not None:
+                if self.w2 == "host" and st.pinned is not None:
                     st.dp.copy_(st.dp_pinned, non_blocking=True)
                 topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dmask, interp=self.interp)
             dlow = postproc_backward(st.dmask.view(B * N, H, W), 256, st.crop, st.orig)
             self.model.mask_decoder.backward_impl(st.saved, dlow.view(B, N, 1, 256, 256))
         loss = st.loss_out
         loss[0:2] = st.loss3[0:2]
-        if st.pinned is not None:
+        if self.w2 == "device":
+            if st.topo_dev is not None:
+                loss[2:3].copy_(st.topo_loss_dev)
+            else:
+                loss[2:3].zero_()
+        elif st.pinned is not None:
             loss[2:3].copy_(st.topo_pinned, non_blocking=True)
         else:
             loss[2] = st.topo_val
@@ -203,7 +217,9 @@ class FusedTrainStep:
     def _graph_key(self, *ts):
         return tuple((None if t is None else (tuple(t.shape), t.dtype)) for t in ts)
 
-    MAX_GRAPHS = 8  # captured step graphs kept (one per batch shape: B, the prompt count N, prompt kind)
+    # captured step graphs kept (one per batch shape: B, the prompt count N, prompt kind; x2 encoder-lookahead
+    # parities): an epoch of the training loop sees a handful of prompt counts
+    MAX_GRAPHS = 16
 
     def _encoder_set(self, ekey, pixel_values):
         """Captured encoder graph E for one pixel shape and parity: its own memory pool, a static pixel input and
@@ -245,7 +261,7 @@ class FusedTrainStep:
         st = self._state(es["pixel"], gt_u8, input_boxes, input_points, input_labels, crop, orig, global_batch)
         st.emb = es["emb"]
         B, N = gt_u8.shape[:2]
-        if self.topological and self.lamda != 0.0:
+        if self.topological and self.lamda != 0.0 and self.w2 == "host":
             entries, maps, midx = topo_index(B, N, self.topo_mode, global_batch, dev)
             Kn = len(maps)
             if Kn:
@@ -275,8 +291,7 @@ class FusedTrainStep:
             st.pinned = None
             st.topo_dev = None
         static = (None, gt_u8, input_boxes, input_points, input_labels)  # pixels: the encoder set's input
-        g = {"graphs": (gf, gf2, gb), "eset": es, "st": st, "ev": torch.cuda.Event(), "static": static,
-             "src": tuple(self._src_tag(t) for t in inputs)}
+        g = {"graphs": (gf, gf2, gb), "eset": es, "st": st, "ev": torch.cuda.Event(), "static": static}
         self._graphs[key] = g
         while len(self._graphs) > self.MAX_GRAPHS:
             self._graphs.pop(next(iter(self._graphs)))
@@ -296,20 +311,17 @@ class FusedTrainStep:
         return a[0] is b[0] and a[1] == b[1]
 
     def _copy_in(self, g, inputs):
-        """Copy a new batch into the captured graphs' static inputs (skipped for the tensors that were copied
-        last and have not changed since: same storage, same version counter)."""
-        tags = tuple(self._src_tag(t) for t in inputs)
-        for dst, src, tag, old in zip(g["static"], inputs, tags, g["src"]):
-            if dst is not None and src is not None and not self._same(tag, old):
+        """Copy the batch into the captured graphs' static inputs — every step: an unchanged tensor object is no
+        proof of unchanged contents (the library's kernels write through raw pointers without bumping torch's
+        version counter), and the copies cost ~10 us of HBM time per step."""
+        for dst, src in zip(g["static"], inputs):
+            if dst is not None and src is not None:
                 dst.copy_(src, non_blocking=True)
-        g["src"] = tags
 
     @staticmethod
     def _pixel_in(es, px):
-        tag = FusedTrainStep._src_tag(px)
-        if not FusedTrainStep._same(tag, es["src"]):
-            es["pixel"].copy_(px, non_blocking=True)
-            es["src"] = tag
+        es["pixel"].copy_(px, non_blocking=True)
+        es["src"] = FusedTrainStep._src_tag(px)
 
     def _graph_forward_backward(self, pixel_values, gt_u8, input_boxes, input_points, input_labels, crop, orig,
                                 global_batch, between=None, next_inputs=None):
@@ -321,7 +333,6 @@ class FusedTrainStep:
         g = self._graphs.get(key + (par,))
         if g is None:
             g = self._capture(key + (par,), inputs, crop, orig, global_batch, ekey)
-            g["src"] = (None,) * 5  # the capture ran on clones: copy this batch in like any other
         es = g["eset"]
         gf, gf2, gb = g["graphs"]
         st, ev = g["st"], g["ev"]
@@ -636,52 +647,74 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     tds = data.SAMDataset(train_data, config, epoch_seed=config.get("data_seed"))
     vds = data.SAMDataset(valid_data, config, epoch_seed=config.get("data_seed"))
     bs = int(config.get("batch_size", 2))
-    # config "graphs" / "pipeline" (off by default): hipGraph replay per batch shape, and the encoder lookahead
-    # (the next batch is built before this step so its encoder can run during this step's decoder)
-    graphs = bool(config.get("graphs", False)) and device.type == "cuda"
+    # config "graphs" / "pipeline" (default on for a GPU; the CLI's --graphs / --pipeline): hipGraph replay per
+    # batch shape, and the encoder lookahead (the next batch is built before this step so its encoder runs during
+    # this step's decoder) — the path bench.py times
+    graphs = _bool_flag(config.get("graphs", True)) and device.type == "cuda"
     step = FusedTrainStep(model, lr=config.get("learning_rate", 1e-3), weight_decay=config.get("weight_decay", 0.0),
                           topological=bool(config.get("topological", False)),
                           topo_mode=config.get("topo_mode", "first"), process_group=pg, graphs=graphs,
-                          pipeline=graphs and bool(config.get("pipeline", False)))
-    hist = {"train_loss": [], "valid_loss": []}
+                          pipeline=graphs and _bool_flag(config.get("pipeline", True)))
+    hist = {"train_loss": [], "valid_loss": [], "train_time_s": []}
+    # the data path (host RNG draws, device components / processor, their host syncs) runs on a side stream, so
+    # building the next batches overlaps the queued steps on the main stream
+    main = torch.cuda.current_stream(device) if device.type == "cuda" else None
+    side = torch.cuda.Stream(device=device) if device.type == "cuda" else None
 
     def build(bi, idx):
         n_glob = len(tds) - bi * bs * world if bi == len(batches) - 1 else bs * world
         n_glob = min(n_glob, bs * world)
-        prep = _prep(tds, idx, prompt, device, device_data)
-        N = _collective_max(prep[2], pg)
-        return n_glob, (_finish(prep, processor, prompt, N, device) if idx else None)
+        if side is None:
+            prep = _prep(tds, idx, prompt, device, device_data)
+            N = _collective_max(prep[2], pg)
+            return n_glob, (_finish(prep, processor, prompt, N, device) if idx else None), None
+        with torch.cuda.stream(side):  # allocations come from the side stream's pool (no wait on queued steps)
+            prep = _prep(tds, idx, prompt, device, device_data)
+            N = _collective_max(prep[2], pg)
+            b = _finish(prep, processor, prompt, N, device) if idx else None
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for v in (b or {}).values():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v.record_stream(main)
+        return n_glob, b, ev
+
+    def inputs_of(b):
+        return (b["pixel_values"], b["gt_u8"], b.get("input_boxes"), b.get("input_points"), b.get("input_labels"))
 
     for epoch in range(int(config.get("epochs", 10))):
         tds.epoch = epoch
         batches = global_batches(len(tds), bs, world, rank, bool(config.get("shuffle", False)),
                                  config.get("data_seed") or 0, epoch)
-        epoch_loss = 0.0
+        t_epoch = time.perf_counter()
+        # sum over steps of loss * images / global images on the device: no per-step host sync (the reference's
+        # .item() of :69 only feeds this sum); one read per epoch
+        loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
         nxt = build(1, batches[1]) if len(batches) > 1 else None
         for bi, idx in enumerate(batches):
             if bi == 0:  # training_utils.py:40-44: the first batch of every epoch is skipped
                 continue
-            n_glob, batch = nxt
+            n_glob, batch, ev = nxt
             # same batch order and RNG draws as building each batch at its own step (the builds stay in order)
             nxt = build(bi + 1, batches[bi + 1]) if bi + 1 < len(batches) else None
             if idx:
+                if ev is not None:
+                    main.wait_event(ev)
                 crop = tuple(int(v) for v in batch["reshaped_input_sizes"][0])
                 orig = tuple(int(v) for v in batch["original_sizes"][0])
                 nb = nxt[1] if (nxt is not None and step.pipeline) else None
-                nxt_in = None if nb is None else (nb["pixel_values"], nb["gt_u8"], nb.get("input_boxes"),
-                                                  nb.get("input_points"), nb.get("input_labels"))
-                loss = step.forward_backward(batch["pixel_values"], batch["gt_u8"],
-                                             input_boxes=batch.get("input_boxes"),
+                if nb is not None and nxt[2] is not None:
+                    main.wait_event(nxt[2])
+                loss = step.forward_backward(*inputs_of(batch)[:2], input_boxes=batch.get("input_boxes"),
                                              input_points=batch.get("input_points"), crop=crop, orig=orig,
-                                             global_batch=n_glob, next_inputs=nxt_in)
-                lv = loss[3].double().cpu() * len(idx)
+                                             global_batch=n_glob, next_inputs=None if nb is None else inputs_of(nb))
+                loss_acc += loss[3:4].double() * len(idx) / n_glob
             else:  # nothing on this rank in a ragged last batch: contribute zero gradient
                 model.mask_decoder.flat_grad.zero_()
-                lv = torch.zeros((), dtype=torch.float64)
             step._launch_update(len(idx), n_glob)  # all-reduce (overlapped with the next encoder forward) + Adam
-            epoch_loss += float(_collective_sum(lv.reshape(1), pg)[0]) / n_glob  # the .item() of :69
         step.flush()
-        epoch_loss /= len(batches)
+        epoch_loss = float(_collective_sum(loss_acc, pg)[0]) / len(batches)
+        hist["train_time_s"].append(time.perf_counter() - t_epoch)
         vloss = validate_model(step, vds, processor, bs, config, world, rank, pg, device, device_data)
         hist["train_loss"].append(epoch_loss)
         hist["valid_loss"].append(vloss)
@@ -815,6 +848,11 @@ def build_parser():
     p.add_argument("--synthetic", type=int, default=0, help="train on K synthetic images (no dataset on disk)")
     p.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp16"],
                    help="16-bit operand type of the frozen image encoder (build extension; fp16 = configs[4])")
+    p.add_argument("--graphs", nargs="?", const=True, default=True, type=_bool_flag,
+                   help="replay each batch shape's step as hipGraphs (default on; --graphs=False: eager launches)")
+    p.add_argument("--pipeline", nargs="?", const=True, default=True, type=_bool_flag,
+                   help="encoder lookahead: the next batch's frozen encoder runs during this step's decoder "
+                        "(default on; needs --graphs)")
     return p
 
 
@@ -837,7 +875,7 @@ def main(argv=None):
               "learning_rate": args.lr, "weight_decay": args.weight_decay, "epochs": args.epochs,
               "batch_size": args.bs, "shuffle": args.shuffle, "optimizer": args.optimizer, "loss": args.loss,
               "time": now, "evaluate": args.evaluate, "topological": args.top, "prompt_type": args.prompt,
-              "pseudocolor": None, "encoder_dtype": args.precision}
+              "pseudocolor": None, "encoder_dtype": args.precision, "graphs": args.graphs, "pipeline": args.pipeline}
     pg = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:

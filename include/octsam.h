@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 12
+#define OCTSAM_ABI_VERSION 13
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -295,7 +295,7 @@ int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int32_t out_h, 
  * ref:octsam/models/topological_loss.py:33-46: pred = interp(f(masks[map_idx[k]]), out_h x out_w,
  * bilinear, align_corners=True) with f = sigmoid (training_utils.py:64) when apply_sigmoid, else identity;
  * gt_out likewise from uint8 gt; octsam_topo_bwd adds scale * d(interp o f)^T dpred into dmask.
- * Persistence: octsam_cubical_ph; Wasserstein: octsam_w2_host. */
+ * Persistence: octsam_cubical_ph; Wasserstein: octsam_topo_w2 (device) or octsam_w2_host. */
 int octsam_topo_down(const float* masks, const uint8_t* gt, const int32_t* map_idx, int32_t K, int32_t in_h,
                      int32_t in_w, int32_t out_h, int32_t out_w, int32_t apply_sigmoid, float* pred, float* gt_out,
                      void* stream);
@@ -315,6 +315,19 @@ int octsam_w2_host(const float* d1_host, int32_t n, const float* d2_host, int32_
 int octsam_topo_host(const int32_t* pairs, const int32_t* cnt, const float* vals, int32_t Kn, int32_t max_pairs,
                      int32_t nvals, const int32_t* entry_maps, const int32_t* entry_off, int32_t n_entries,
                      int32_t feat_col, double q, double lamda, int32_t want_grad, double* loss_out, float* dpred);
+
+/* The same loss and gradient on the DEVICE: no host round trip between the step's forward
+ * and backward. Inputs as octsam_topo_host (device pointers) plus map_entry [Kn] = the entry holding map k
+ * (-1 = none). Writes loss_out[0] (NaN if a pair count exceeds max_pairs) and, if want_grad, dpred [Kn, nvals]
+ * (every row written). Per map one wave solves the diagonal-augmented assignment with the host's
+ * shortest-augmenting-path Hungarian method (lowest column on ties), so loss and gradient are bit-identical to
+ * octsam_topo_host at q = 2. workspace: octsam_topo_w2_workspace(Kn, max_pairs) bytes.
+ * Replaces torch_topological WassersteinDistance -> POT ot.emd2 + ref:octsam/models/topological_loss.py:68-96. */
+int64_t octsam_topo_w2_workspace(int32_t Kn, int32_t max_pairs);
+int octsam_topo_w2(const int32_t* pairs, const int32_t* cnt, const float* vals, int32_t Kn, int32_t max_pairs,
+                   int32_t nvals, const int32_t* entry_maps, const int32_t* entry_off, const int32_t* map_entry,
+                   int32_t n_entries, int32_t feat_col, double q, double lamda, int32_t want_grad, void* workspace,
+                   int64_t workspace_bytes, double* loss_out, float* dpred, void* stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.Adam step over a flat fp32 buffer (ref:octsam/models/training_utils.py:31,68):

@@ -50,10 +50,20 @@ class CpuReferenceStep:
         self.topo_mode = topo_mode
         self.loss_device = torch.device(loss_device)
 
-    def predict(self, batch):
-        """Post-processed fp32 logits [B, N, H, W] on loss_device (training_utils.py:56-58 / :121-125)."""
+    @torch.no_grad()
+    def embed(self, batch):
+        """Image embeddings of the frozen encoder (the vision encoder has no trainable weight, so a batch's
+        embedding is the same at every step: callers may compute it once and pass it to predict/step)."""
+        return self.model.get_image_embeddings(batch["pixel_values"].float().to(self.device))
+
+    def predict(self, batch, image_embeddings=None):
+        """Post-processed fp32 logits [B, N, H, W] on loss_device (training_utils.py:56-58 / :121-125).
+        image_embeddings: the frozen encoder's output for this batch (embed()), or None to run the encoder."""
         dev = self.device
-        inputs = {"pixel_values": batch["pixel_values"].float().to(dev)}
+        if image_embeddings is not None:
+            inputs = {"image_embeddings": image_embeddings}
+        else:
+            inputs = {"pixel_values": batch["pixel_values"].float().to(dev)}
         if "input_boxes" in batch:
             inputs["input_boxes"] = batch["input_boxes"].to(dev)
         if "input_points" in batch:
@@ -66,9 +76,9 @@ class CpuReferenceStep:
         masks = masks[..., :rh, :rw]
         return F.interpolate(masks, (oh, ow), mode="bilinear", align_corners=False)
 
-    def forward_loss(self, batch):
+    def forward_loss(self, batch, image_embeddings=None):
         gt = batch["gt_u8"].to(self.loss_device).double()
-        masks = self.predict(batch)
+        masks = self.predict(batch, image_embeddings)
         loss = dicece_ref(masks, gt)
         topo = torch.zeros((), dtype=torch.float64)
         if self.topological:
@@ -77,9 +87,9 @@ class CpuReferenceStep:
             loss = loss + topo
         return loss, topo, masks
 
-    def step(self, batch):
+    def step(self, batch, image_embeddings=None):
         self.opt.zero_grad()
-        loss, topo, _ = self.forward_loss(batch)
+        loss, topo, _ = self.forward_loss(batch, image_embeddings)
         loss.backward()
         self.opt.step()
         return float(loss.item())

@@ -2,6 +2,8 @@
 formulation it replaced (kept here as the checker: octsam_w2_host per map pair, numpy accumulation),
 on random diagrams with empty, tiny and large pred / gt diagrams, grouped entries ("all" mode) and a
 zero-cost entry (inf * 0 -> nan gradient, as torch's pow backward gives). Bit-identical loss and gradient."""
+import math
+
 import numpy as np
 import pytest
 
@@ -32,9 +34,13 @@ def _reference(pairs_h, cnt_h, vals_h, entries, maps, lamda=0.1, feat_d=1, loss_
             costs.append(c)
             grads.append((k, pr1, g))
         tot = float(np.float32(sum(costs)))
-        total += tot ** (1.0 / loss_q)
+        # q = 2: sqrt for the 1/q power (correctly rounded, the same bits on the host and the device)
+        total += math.sqrt(tot) if loss_q == 2 else tot ** (1.0 / loss_q)
         if want_grad:
-            dd = (1.0 / loss_q) * (tot ** (1.0 / loss_q - 1.0)) if tot > 0 else float("inf")
+            if tot > 0:
+                dd = 0.5 / math.sqrt(tot) if loss_q == 2 else (1.0 / loss_q) * (tot ** (1.0 / loss_q - 1.0))
+            else:
+                dd = float("inf")
             for k, pr1, g in grads:
                 if len(pr1) == 0:
                     continue
