@@ -64,7 +64,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
                    help="16-bit operand type of the frozen encoder (fp16: BASELINE configs[4]); the decoder is bf16")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle step (rank 0, N=1)")
-    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--cpu-batch8", type=int, default=1, help="also time one CPU oracle step of the full batch")
     p.add_argument("--val", type=int, default=8, help="val images for the Dice readout (0 = skip)")
     p.add_argument("--data-path", type=int, default=1,
                    help="time building one batch on the host (reference data path) vs the HIP data path")
@@ -77,6 +78,8 @@ def parse():
     p.add_argument("--e2e-steps", type=int, default=10,
                    help="steps of the end-to-end loop (a new batch per step through the HIP data path)")
     p.add_argument("--topo-all", type=int, default=1, help="time the topo_mode='all' reading of batch_iter too")
+    p.add_argument("--loop-images", type=int, default=128,
+                   help="time train.training() over an epoch of this many synthetic images (0 = skip)")
     return p.parse_args()
 
 
@@ -301,7 +304,7 @@ def end_to_end(args, step, device, rank, world, pg, n_raw=4):
         with torch.cuda.stream(side):
             b = collate_device(imgs, labs, args.prompt, device, seed_hooks=hooks, processor=dproc)
             b.pop("prompt_raw")
-            if world > 1:  # global-N padding (a tiny MAX all-reduce on the main process group)
+            if pg is not None:  # global-N padding (a tiny MAX all-reduce on the main process group)
                 b = _pad_global(b, pg, device)
             ev = torch.cuda.Event()
             ev.record(side)
@@ -361,48 +364,102 @@ def _pad_global(b, pg, device):
 
 def topo_all_sensitivity(args, model, batch, steps=5):
     """ms/step with the topo_mode='all' reading of torch_topological's batch_iter (every prompt's diagrams,
-    2*B*N persistence maps per step instead of 2*B; SURVEY.md §8(a) A17 — the reading is unpinned)."""
+    2*B*N persistence maps per step instead of 2*B; SURVEY.md §8(a) A17 — the reading is unpinned), with the
+    transport on the device (the step's default, octsam_topo_w2) and on the host between the graphs (w2_host:
+    octsam_topo_host after a device sync, the round-2 path) for comparison."""
     from dilabhelmholtzoct_amd.train import FusedTrainStep
     pipe = bool(args.pipeline) and not args.eager
-    st = FusedTrainStep(model, lr=1e-3, topological=True, topo_mode="all", graphs=not args.eager, pipeline=pipe)
-    for i in range(2):
-        st.step(batch, next_batch=batch if i == 0 else None)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        st.step(batch, next_batch=batch if i + 1 < steps else None)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
     B, N = batch["gt_u8"].shape[:2]
-    out = {"ms_per_step": round(dt * 1e3 / steps, 3), "imgs_per_s": round(B * steps / dt, 2),
-           "persistence_maps_per_step": 2 * B * N, "steps": steps}
+    out = {"persistence_maps_per_step": 2 * B * N, "entries": B, "steps": steps}
+    for w2 in ("device", "host"):
+        st = FusedTrainStep(model, lr=1e-3, topological=True, topo_mode="all", graphs=not args.eager, pipeline=pipe,
+                            w2=w2)
+        for i in range(2):
+            st.step(batch, next_batch=batch if i == 0 else None)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            st.step(batch, next_batch=batch if i + 1 < steps else None)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        key = "" if w2 == "device" else "w2_host_"
+        out[key + "ms_per_step"] = round(dt * 1e3 / steps, 3)
+        out[key + "imgs_per_s"] = round(B * steps / dt, 2)
+        del st
     log(f"topo_mode=all: {out}")
     return out
 
 
+def time_training_loop(args, device, n_images=128):
+    """The drop-in loop itself (train.training, ref:octsam/models/training.py:184 -> training_utils.py:27-80) over a
+    synthetic n_images-image epoch: its defaults (hipGraphs + encoder lookahead, HIP data path on a side stream),
+    the first-batch skip included; timed over the second epoch's training pass (the first captures the graphs),
+    validation and evaluation excluded. value = images trained / epoch time."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.train import training
+    cfg = {"batch_size": args.batch, "epochs": 2, "learning_rate": 1e-3, "topological": bool(args.top),
+           "prompt_type": args.prompt, "evaluate": False, "checkpoint": None, "data_seed": 0, "seed": 0,
+           "encoder_dtype": args.dtype}
+    hist = training(args.model, cfg, data.synthetic_oct(seed=4000, n=n_images),
+                    data.synthetic_oct(seed=4001, n=args.batch), device=device, log=lambda *a: None)
+    t = hist["train_time_s"][-1]
+    trained = n_images - args.batch  # training_utils.py:40-44 skips each epoch's first batch
+    out = {"value": round(trained / t, 2), "unit": "imgs/s", "epoch_s": round(t, 4), "images_trained": trained,
+           "loader_images": n_images, "train_loss": hist["train_loss"],
+           "note": "train.training() defaults (graphs + lookahead, HIP data path); 2nd epoch's training pass"}
+    log(f"training loop: {out['value']} imgs/s ({t * 1e3:.1f} ms per {n_images}-image epoch)")
+    return out
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args, batch_cpu):
-    """CPU oracle step (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE/topo + Adam) on a
-    bounded sample (1 image, all its prompts), timed on this host's cores."""
+    """CPU oracle step (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE/topo + Adam) timed on
+    this host's cores: the headline sample is batch 1 (one image, all its prompts) with the
+    bench's --top, 1 warm-up + cpu_steps timed steps; beside it batch 1 with the other --top setting
+    (configs[0] is top off) and one batch-8 step (configs[1]/[2]'s batch) — bounded, so the default bench
+    finishes in minutes."""
     from oracle.step_ref import CpuReferenceStep
     # the GPU box shows the whole machine's CPUs; this job's share is OMP_NUM_THREADS (16 there)
     ncores = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     ncores = min(ncores, share) if share > 0 else min(ncores, 16)
     torch.set_num_threads(ncores)
-    step = CpuReferenceStep(args.model, topological=bool(args.top), seed=0)
+
+    def timed(top, b, steps, warm):
+        step = CpuReferenceStep(args.model, topological=top, seed=0)
+        for _ in range(warm):
+            step.step(b)
+        t0 = time.time()
+        for _ in range(steps):
+            step.step(b)
+        dt = time.time() - t0
+        log(f"cpu baseline: batch {int(b['gt_u8'].shape[0])} top={top}: {dt / steps:.2f} s/step")
+        return int(b["gt_u8"].shape[0]) * steps / dt
+
     one = {k: (v[:1] if isinstance(v, torch.Tensor) and v.dim() > 0 else v) for k, v in batch_cpu.items()}
-    step.step(one)  # warm-up
-    log(f"cpu baseline: warm-up done on {ncores} threads")
-    t0 = time.time()
-    for _ in range(args.cpu_steps):
-        step.step(one)
-        log(f"cpu baseline: step {time.time() - t0:.1f} s")
-    dt = time.time() - t0
+    value = timed(bool(args.top), one, args.cpu_steps, 1)
+    points = [{"batch": 1, "top": not bool(args.top), "steps": args.cpu_steps,
+               "imgs_per_s": round(timed(not bool(args.top), one, args.cpu_steps, 1), 5)}]
+    if args.cpu_batch8:
+        points.append({"batch": int(batch_cpu["gt_u8"].shape[0]), "top": bool(args.top), "steps": 1,
+                       "imgs_per_s": round(timed(bool(args.top), batch_cpu, 1, 0), 5)})
     n_prompts = int(one["gt_u8"].shape[1])
-    return {"value": round(args.cpu_steps / dt, 5), "unit": "imgs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of batch 1 ({n_prompts} {args.prompt}), fp32, "
-                      f"oracle/step_ref.py on {ncores} host threads"}
+    return {"value": round(value, 5), "unit": "imgs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of batch 1 ({n_prompts} {args.prompt}), "
+                      f"--top={bool(args.top)}, fp32, oracle/step_ref.py on {ncores} host threads",
+            "points": points}
 
 
 def _free_port() -> int:
@@ -444,7 +501,7 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if world > 1 or "WORLD_SIZE" in os.environ:  # a launcher's ranks (torchrun; world 1 included): RCCL
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
         pg = dist.group.WORLD
@@ -454,7 +511,7 @@ def main():
 
     processor = data.make_processor()
     batch_cpu = make_batch(args, rank, device, processor)
-    if world > 1:  # global-N padding: every rank pads prompts to the global max (single-process collate)
+    if pg is not None:  # global-N padding: every rank pads prompts to the global max (single-process collate)
         import torch.distributed as dist
         n = torch.tensor([batch_cpu["gt_u8"].shape[1]], device=device)
         dist.all_reduce(n, op=dist.ReduceOp.MAX)
@@ -594,6 +651,9 @@ def main():
     topo_all = None
     if args.topo_all and args.top and rank == 0 and world == 1:
         topo_all = topo_all_sensitivity(args, model, batch)
+    loop = None
+    if args.loop_images and rank == 0 and world == 1 and not args.eager:
+        loop = time_training_loop(args, device, args.loop_images)
 
     log(f"rank {rank}: {dt * 1e3 / args.steps:.2f} ms/step")
     val_dice = val_metrics = None
@@ -630,6 +690,7 @@ def main():
             "config": {"workload": workload_name(args), "model": args.model, "global_batch": args.batch * world,
                        "prompts_per_image": N, "prompt": args.prompt, "top": bool(args.top),
                        "parallelism": f"dp{world}",
+                       "process_group": None if pg is None else "nccl",
                        "exec": "eager" if args.eager else
                        ("hipgraph + encoder lookahead (next step's frozen encoder on a side stream during this "
                         "step's decoder; each timed step runs its own encoder)" if pipe else "hipgraph")},
@@ -640,6 +701,7 @@ def main():
             "data_path": data_path,
             "value_end_to_end": e2e["value"] if e2e else None,
             "end_to_end": e2e,
+            "training_loop": loop,
             "topo_mode_all": topo_all,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -82,7 +82,7 @@ def test_decoder_forward_backward(cuda, models, prompt):
     ref_g = {n: p.grad for n, p in hf.mask_decoder.named_parameters()}
     ref_b = {n: p.grad for n, p in hfb.mask_decoder.named_parameters()}
     scale = max(g.norm().item() for g in ref_g.values() if g is not None)
-    bad = {}
+    bad, errs = {}, {}
     for n, p in ours.mask_decoder.named_parameters():
         r = ref_g[n]
         if r is None or r.norm().item() < 1e-6 * scale:
@@ -91,8 +91,11 @@ def test_decoder_forward_backward(cuda, models, prompt):
             continue
         e = _rel(p.grad, r)
         eb = _rel(ref_b[n].float(), r)
+        errs[n] = (e, eb)
         if e > max(0.05, min(0.25, eb + 0.02)):
             bad[n] = (e, eb)
+    worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:6]
+    print("worst per-tensor rel err (ours, hf-bf16):", [(n, round(a, 4), round(b, 4)) for n, (a, b) in worst])
     assert not bad, bad
 
 
