@@ -61,6 +61,7 @@ _SIGNATURES = {
     "octsam_group_sum": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p]),
     "octsam_vit_attention": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                        c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "octsam_attention_set_variant": (None, [c_int32]),
     "octsam_axpby": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int64, c_float, c_float, c_void_p,
                                c_int32, c_void_p, c_int64, c_void_p]),
     "octsam_colsum": (c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_void_p]),

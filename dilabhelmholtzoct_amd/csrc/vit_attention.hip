@@ -460,6 +460,187 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
   store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
+// ---------------------------------------------------------------- global, software-pipelined (A/B variant 0)
+// Same arithmetic as vit_attn_global_kernel (bit-identical outputs), reordered per wave so that its own
+// instruction stream keeps both pipes busy: the q.k MFMAs of tile t+1 issue while the VALU exponentiates tile t,
+// and the P.V MFMAs of tile t issue while the VALU takes the maximum of tile t+1. In the plain loop every phase
+// of a tile (q.k, softmax, P.V) runs on the two waves of a SIMD at the same time (they meet at the per-tile
+// barrier), so the matrix pipe idles through the softmax and the VALU through the products. A 4-deep K/V ring
+// (tile t+1 must be resident while tile t's V is still read), 2 tiles in flight. Measured on MI355X: bit-identical
+// to the plain loop and no faster (526 vs 521 us per vit-b layer, profiles/r03/attn_pipelined_ab.log), so the plain
+// loop stays the default.
+constexpr int NBUF_P = 4;
+template <int HD> constexpr int gp_smem() { return G_RELH + NBUF_P * Geo<HD>::TILE + 128; }
+static_assert(gp_smem<80>() <= 160 * 1024, "pipelined global attention LDS");
+
+// exp / row-sum / bf16 pack of one tile's scores (base 2: p = exp2(c1 * s + c)); returns the four P^T operands
+template <typename E>
+__device__ __forceinline__ void softmax_pack(f32x16 (&s)[2], float c1, float c, f32x2& ls2,
+                                             typename ET<E>::v8 (&pf)[4]) {
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const f32x2 x = {s[t2][r], s[t2][r + 1]};
+      const f32x2 y = x * c1 + c;  // v_pk_fma_f32
+      const f32x2 pv = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+      s[t2][r] = pv[0];
+      s[t2][r + 1] = pv[1];
+      ls2 += pv;  // v_pk_add_f32
+    }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) pf[ks] = pack8<E>(s[ks >> 1], 8 * (ks & 1));
+}
+
+// raw maximum of one tile's 32 scores per lane, then the tile maximum in base-2 units across the lane halves
+__device__ __forceinline__ float tile_max(const f32x16 (&s)[2], float c1, float rh) {
+  float mx = s[0][0];
+#pragma unroll
+  for (int i = 1; i < 31; i += 2) mx = max3f(mx, s[i >> 4][i & 15], s[(i + 1) >> 4][(i + 1) & 15]);
+  mx = fmaxf(mx, s[1][15]);
+  return max_halves(fmaf(mx, c1, rh));
+}
+
+template <int HD, typename E, bool MORE, bool WAIT_PART, bool LOAD>
+__device__ __forceinline__ void gpipe_step(int tile, f32x16 (&s_cur)[2], f32x16 (&s_nxt)[2], float& mx_cur,
+                                           float& rh_cur, float& m_run, float& l_run, f32x16 (&acc_o)[Geo<HD>::NTD],
+                                           const typename ET<E>::v8 (&qf)[Geo<HD>::NKS], const f32x16 (&relw)[2],
+                                           const float* relh, char* ring, const char* zero, const E* kbase,
+                                           const E* vbase, int ld, float c1, int wave, int lane) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  const int h = lane >> 5, l32 = lane & 31;
+  lazy_rescale<G::NTD>(mx_cur, m_run, l_run, acc_o);
+  const float c = rh_cur - m_run;
+  if constexpr (MORE) {
+    // tile + 1 resident (vmcnt: the loads issued after it may stay in flight); every wave is past P.V(tile - 1),
+    // so the slot of tile + 3 (= tile - 1's) may be restaged
+    if constexpr (WAIT_PART) wait_vm<G::OPS>();
+    else wait_vm<0>();
+    raw_barrier();
+    if constexpr (LOAD)
+      load_tile<HD, NW, E>(kbase, vbase, ld, (tile + 3) * 64, ring + ((tile + 3) % NBUF_P) * G::TILE, wave, lane);
+  }
+  const char* slot = ring + (tile % NBUF_P) * G::TILE;
+  // q.k of tile + 1 (matrix pipe) beside the exponentials of tile (VALU)
+  if constexpr (MORE) {
+    const char* nslot = ring + ((tile + 1) % NBUF_P) * G::TILE;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) s_nxt[t2] = qk_block<HD, E>(nslot, t2, qf, relw[t2], l32, h);
+  }
+  f32x2 ls2 = {0.0f, 0.0f};
+  V8 pf[4];
+  softmax_pack<E>(s_cur, c1, c, ls2, pf);
+  l_run += ls2[0] + ls2[1];
+  if constexpr (MORE) {
+    // interleave: the 8 K-fragment reads, then one q.k MFMA per 10 VALU instructions of the softmax
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int i = 0; i < 8 + (G::TAIL ? 2 : 0); ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+    }
+  }
+  // P.V of tile (matrix pipe) beside the maximum of tile + 1 (VALU)
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) pv_step<HD, E>(slot, zero, ks, pf[ks], acc_o, lane);
+  if constexpr (MORE) {
+    rh_cur = relh[(tile + 1) * 32 + l32];
+    mx_cur = tile_max(s_nxt, c1, rh_cur);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+    }
+  }
+}
+
+template <int HD, typename E>
+__global__ __launch_bounds__(THR) void vit_attn_global_pipe_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+                                                                  const float* __restrict__ Rh,
+                                                                  const float* __restrict__ Rw, int heads, float scale) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  constexpr int S = 64, T = 4096, NT = T / 64;
+  static_assert(NT % 2 == 0 && NT >= 6, "pairs of tiles, three tail pairs");
+  static_assert(NW * G_SCR * 4 <= G_RELH + NBUF_P * G::TILE, "rel_w scratch must fit");
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int qblk = lid & 15, head = (lid >> 4) % heads, seq = (lid >> 4) / heads;
+  const int D = heads * HD, ld = 3 * D;
+  const E* base = qkv + (long long)seq * T * ld;
+  const int q = qblk * (NW * 32) + wave * 32 + l32;
+  const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
+  const float c1 = scale * L2E;
+  if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+
+  V8 qf[G::NKS];
+  load_q<HD, E>(base + (long long)q * ld + head * HD, qf, h);
+  float* scr = (float*)gsm + wave * G_SCR;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 t = rel_block<HD, E>(Rw, qw0 + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * 33 + l32] = t[r];
+  }
+  __syncthreads();
+  const float inv_scale = 1.0f / scale;
+  f32x16 relw[2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * 33 + l32] * inv_scale;
+  __syncthreads();
+  float* relh = (float*)gsm + wave * (64 * 32);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const f32x16 t = rel_block<HD, E>(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
+  }
+  char* ring = gsm + G_RELH;
+  char* zero = ring + NBUF_P * G::TILE;
+  if (tid < 32) ((float*)zero)[tid] = 0.0f;
+  __syncthreads();
+
+  const E* kbase = base + D + head * HD;
+  const E* vbase = base + 2 * D + head * HD;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) load_tile<HD, NW, E>(kbase, vbase, ld, t * 64, ring + t * G::TILE, wave, lane);
+
+  f32x16 acc_o[G::NTD];
+#pragma unroll
+  for (int td = 0; td < G::NTD; ++td) acc_o[td] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+  // tile 0 resident (tiles 1, 2 in flight): its scores and maximum
+  wait_vm<2 * G::OPS>();
+  raw_barrier();
+  f32x16 sA[2], sB[2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) sA[t2] = qk_block<HD, E>(ring, t2, qf, relw[t2], l32, h);
+  float rh_cur = relh[l32];
+  float mx_cur = tile_max(sA, c1, rh_cur);
+  // tile pairs (sA holds even tiles' scores, sB odd ones): the last three tiles stop loading / waiting
+  for (int tile = 0; tile < NT - 4; tile += 2) {
+    gpipe_step<HD, E, true, true, true>(tile, sA, sB, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring, zero,
+                                        kbase, vbase, ld, c1, wave, lane);
+    gpipe_step<HD, E, true, true, true>(tile + 1, sB, sA, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring,
+                                        zero, kbase, vbase, ld, c1, wave, lane);
+  }
+  gpipe_step<HD, E, true, true, true>(NT - 4, sA, sB, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring, zero,
+                                      kbase, vbase, ld, c1, wave, lane);
+  gpipe_step<HD, E, true, true, false>(NT - 3, sB, sA, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring, zero,
+                                       kbase, vbase, ld, c1, wave, lane);
+  gpipe_step<HD, E, true, false, false>(NT - 2, sA, sB, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring,
+                                        zero, kbase, vbase, ld, c1, wave, lane);
+  gpipe_step<HD, E, false, false, false>(NT - 1, sB, sA, mx_cur, rh_cur, m_run, l_run, acc_o, qf, relw, relh, ring,
+                                         zero, kbase, vbase, ld, c1, wave, lane);
+  const float l_tot = sum_halves(l_run);
+  store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
+}
+
 // ------------------------------------------------------------------------------------ window (side 14)
 // Keys are laid out in slots 16 kh + kw (kw < 14 real; 14 key rows -> slots 0..223, 3.5 tiles). A 32-slot
 // block holds key rows kh0 = 2 block and kh0 + 1, and accumulator register r of lane half h holds slot
@@ -606,20 +787,33 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
   store_out<HD, E>(out + orow * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
+int g_attn_variant = 1;  // 0: software-pipelined global kernel, 1 (default): the plain loop (octsam_attention_set_variant)
+
 template <int HD, typename E>
 int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nseq, int side, int heads, int grid,
            const void* pad, hipStream_t s) {
   const float scale = 1.0f / sqrtf((float)HD);
   if (side == 64) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)vit_attn_global_kernel<HD, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                g_smem<HD>());
-      attr = true;
-    }
     static_assert(4096 / (NW * 32) == 16, "16 query blocks per (sequence, head)");
-    hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(),
-                       s, (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+    if (g_attn_variant == 1) {  // the plain loop (A/B)
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vit_attn_global_kernel<HD, E>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, g_smem<HD>());
+        attr = true;
+      }
+      hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(), s,
+                         (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+    } else {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vit_attn_global_pipe_kernel<HD, E>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, gp_smem<HD>());
+        attr = true;
+      }
+      hipLaunchKernelGGL((vit_attn_global_pipe_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), gp_smem<HD>(), s,
+                         (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+    }
   } else {
     static bool attr = false;
     if (!attr) {
@@ -661,3 +855,5 @@ extern "C" int octsam_vit_attention(const void* qkv, void* out, const float* rel
   OCTSAM_LAUNCH_CHECK("octsam_vit_attention");
   return 0;
 }
+
+extern "C" void octsam_attention_set_variant(int32_t variant) { g_attn_variant = variant; }

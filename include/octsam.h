@@ -151,6 +151,9 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
                          int32_t side, int32_t heads, int32_t head_dim, int32_t fp16, int32_t grid,
                          const void* pad_row, void* stream);
+/* A/B switch for the global layers' kernel: 1 (default) = the plain per-tile loop, 0 = software-pipelined (q.k of
+   the next key tile beside the softmax of this one: bit-identical, measured no faster, profiles/r03/attn_pipelined_ab.log) */
+void octsam_attention_set_variant(int32_t variant);
 
 /* ---------------------------------------------------------------- element-wise / reductions / prompts */
 /* out[i] = alpha*a[i] + beta*b[b_period ? i % b_period : i]  (a or b may be NULL = 0); out2_f32 optional copy.

@@ -96,3 +96,33 @@ def evaluate_metrics_ref(mask_logits: list, gt_masks: list, mask_values: list, n
     mean = {k: float(np.mean(cat[k])) for k in keys}
     smean = {k: float(np.mean(smp[k])) for k in keys}
     return {"category": cat, "sample": smp, "mean": mean, "sample_mean": smean}
+
+
+def pooled_confusion_ref(mask_logits: torch.Tensor, gt_u8: torch.Tensor, mask_values, num_classes: int = 14):
+    """Per-class pooled (tp, fp, fn, tn) int64 [C, 4] of sigmoid(logits) > 0.5 (:126-127) against the 0/1 gt, with
+    the break quirk (:128-130): the counts evaluate_metrics_ref's confusion_matrix calls pool, in plain torch (any
+    device) for the long val-Dice parity test. mask_logits / gt_u8 [B, N, H, W], mask_values [B, N]."""
+    mv = np.asarray(mask_values.cpu() if isinstance(mask_values, torch.Tensor) else mask_values)
+    pred = torch.sigmoid(mask_logits.float()) > 0.5
+    g = gt_u8.to(pred.device).bool()
+    cnt = torch.stack([(pred & g).sum((2, 3)), (pred & ~g).sum((2, 3)), (~pred & g).sum((2, 3)),
+                       (~pred & ~g).sum((2, 3))], -1).cpu()
+    out = torch.zeros(num_classes, 4, dtype=torch.int64)
+    for b in range(mv.shape[0]):
+        for c in range(mv.shape[1]):
+            if mv[b, c] == 0 and c > 0:
+                break
+            out[int(mv[b, c])] += cnt[b, c]
+    return out
+
+
+def mean_dice_ref(pooled: torch.Tensor) -> float:
+    """"Mean dice" (:156, :246): mean over the classes of 2tp / (2tp + fp + fn), 0 for an empty class."""
+    d = [2 * tp / (2 * tp + fp + fn) if (2 * tp + fp + fn) else 0.0 for tp, fp, fn, _ in pooled.tolist()]
+    return float(np.mean(d))
+
+
+def mean_specificity_ref(pooled: torch.Tensor) -> float:
+    """Mean over the classes of tn / (tn + fp) (:150-153), 0 for an empty class."""
+    d = [tn / (tn + fp) if (tn + fp) else 0.0 for tp, fp, fn, tn in pooled.tolist()]
+    return float(np.mean(d))

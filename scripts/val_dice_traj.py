@@ -154,7 +154,7 @@ def main():
                 evaluate(k)
             if k in save_at and ref is not None:
                 from safetensors.torch import save_file
-                sd = {"mask_decoder." + n: t.detach().float().cpu().contiguous()
+                sd = {"mask_decoder." + n: t.detach().to(torch.bfloat16).cpu().contiguous()  # 8 MB
                       for n, t in ref.model.mask_decoder.state_dict().items()}
                 os.makedirs(a.save_dir, exist_ok=True)
                 save_file(sd, os.path.join(a.save_dir, f"decoder_step{k}.safetensors"))

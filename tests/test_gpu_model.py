@@ -92,7 +92,8 @@ def test_decoder_forward_backward(cuda, models, prompt):
         e = _rel(p.grad, r)
         eb = _rel(ref_b[n].float(), r)
         errs[n] = (e, eb)
-        if e > max(0.05, min(0.25, eb + 0.02)):
+        # never less accurate than transformers' own bf16 run of the same decoder (capped at 0.2), floor 0.05
+        if e > max(0.05, min(0.2, eb)):
             bad[n] = (e, eb)
     worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:6]
     print("worst per-tensor rel err (ours, hf-bf16):", [(n, round(a, 4), round(b, 4)) for n, (a, b) in worst])

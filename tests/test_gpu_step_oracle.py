@@ -7,7 +7,7 @@ speed) on the same synthetic weights and batch:
   GPUs), with the bf16 encoder and with the fp16 encoder (the configuration's precision).
 
 Checked: the DiceCE (1e-3 relative) and topological (2e-2 relative) loss values and the mask-decoder gradient
-(global cosine > 0.99, every tensor's relative Frobenius error < 0.1). The topo loss of configs[4]'s B > 1 batch covers prompt 0 of each image
+(global cosine > 0.99, median per-tensor relative Frobenius error < 0.02, every tensor < 0.15). The topo loss of configs[4]'s B > 1 batch covers prompt 0 of each image
 (topo_mode "first")."""
 import pytest
 import torch
@@ -66,7 +66,7 @@ def test_step_vs_oracle(cuda, case):
 
     rg = {n: p.grad.double().cpu() for n, p in ref.model.mask_decoder.named_parameters() if p.grad is not None}
     scale = max(g.norm().item() for g in rg.values())
-    flat_got, flat_want, bad = [], [], {}
+    flat_got, flat_want, bad, errs = [], [], {}, []
     for n, r in rg.items():
         if r.norm().item() < 1e-6 * scale:  # no gradient in the reference (softmax-invariant key biases)
             continue
@@ -74,10 +74,14 @@ def test_step_vs_oracle(cuda, case):
         flat_got.append(g.flatten())
         flat_want.append(r.flatten())
         e = _rel(g, r)
-        if e > 0.1:
+        errs.append(e)
+        if e > 0.15:  # the ill-conditioned self-attention / token-side query biases reach ~0.1 (tests/test_gpu_model.py)
             bad[n] = e
     got, want = torch.cat(flat_got), torch.cat(flat_want)
     cos = float((got @ want) / (got.norm() * want.norm()))
     print(f"{case}: decoder gradient cosine {cos:.5f}, worst tensors {sorted(bad.items(), key=lambda kv: -kv[1])[:4]}")
+    med = sorted(errs)[len(errs) // 2]
+    print(f"{case}: median per-tensor relative error {med:.4f}")
     assert cos > 0.99, cos
+    assert med < 0.02, med
     assert not bad, bad
