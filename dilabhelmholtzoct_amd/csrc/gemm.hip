@@ -618,7 +618,7 @@ __global__ __launch_bounds__(512, 2) void gemm_glds_kernel(GemmK p, int batch) {
   constexpr int CPR = BK / 8, RPI = 64 / CPR;
   constexpr int GL_PER_WAVE = (BM_ / RPI + BN_ / RPI) / 8;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int per_batch = p.tiles_m * p.tiles_n;
   const int ntiles = per_batch * batch;
@@ -1392,7 +1392,7 @@ template <int DBG, int EPI, int FE = 0>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   constexpr bool TR = EPI >= 0;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   int bid = blockIdx.x;
   {
@@ -1678,7 +1678,7 @@ __device__ __forceinline__ void epilogue_n192(const GemmK& p, f32x4 (&acc)[8][3]
 template <int EPI, int FE>
 __global__ __launch_bounds__(512, 2) void gemm8n192_kernel(GemmK p) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   int bid = blockIdx.x;
   {
@@ -1789,6 +1789,139 @@ int launch_gemm8n192(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
   hipLaunchKernelGGL((gemm8n192_kernel<EPI, FE>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Two workgroups per CU: 256x128 tiles, 4 waves (2 M x 2 N; each wave owns 128 x 64 exactly as in gemm8_kernel, so
+// the same lean epilogues apply), K-steps of 32 through a 3-stage LDS-DMA ring (24 KiB per stage, 72 KiB per
+// workgroup, two workgroups per CU). Each SIMD runs one wave of each workgroup and the two workgroups keep their
+// own barriers, so one's epilogue and next-tile prologue (no MFMA) overlap the other's main loop — the 256x256
+// kernel holds the whole CU (128 KiB LDS, 2 x 256 VGPR per SIMD) and leaves its matrix pipes idle through every
+// epilogue (QKV 27 us, MLP1 56 us of 126 / 174, profiles/r02f/gemm_variants_epilogue.log).
+namespace g4 {
+constexpr int KS = 32, NS = 3, A_BYTES = 256 * KS * 2, B_BYTES = 128 * KS * 2, STAGE = A_BYTES + B_BYTES;
+constexpr int LDS = NS * STAGE;
+constexpr int OPS = 6;  // LDS-DMA issues per wave per stage: A 16 KiB + B 8 KiB = 24 x 1 KiB over 4 waves
+
+// per-lane source of each of the wave's 6 issues (16 rows x 64 B per issue, [row][32] image with the 16-B chunk
+// index XOR-swizzled by (row >> 2) & 3 — sw_off<32> — applied to the source: the LDS image stays lane-linear)
+struct Src {
+  const e16* p[OPS];
+};
+__device__ __forceinline__ Src make_src(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int wave,
+                                        int lane) {
+  Src s;
+  const int rr = lane >> 2, slot = lane & 3;
+#pragma unroll
+  for (int u = 0; u < OPS; ++u) {
+    const bool isA = u < 4;
+    const int j = isA ? wave * 4 + u : wave * 2 + (u - 4);
+    const int r = j * 16 + rr;
+    const int c = slot ^ ((r >> 2) & 3);
+    const int lim = isA ? p.M : p.N;
+    int g = (isA ? row0 : col0) + r;
+    g = g < lim ? g : lim - 1;  // rows past M / N: any valid row (never stored)
+    s.p[u] = (isA ? A + (long long)g * p.lda : B + (long long)g * p.ldb) + c * 8;
+  }
+  return s;
+}
+__device__ __forceinline__ void stage(const Src& s, int k0, char* buf, int wave) {
+#pragma unroll
+  for (int u = 0; u < OPS; ++u) {
+    const bool isA = u < 4;
+    const int j = isA ? wave * 4 + u : wave * 2 + (u - 4);
+    __builtin_amdgcn_global_load_lds((const void*)(s.p[u] + k0), (lds_ptr_t)(buf + (isA ? 0 : A_BYTES) + j * 1024), 16,
+                                     0, 0);
+  }
+}
+__device__ __forceinline__ e16x8 frag(const char* img, int row, int kc) {
+  return *(const e16x8*)(img + sw_off<32>(row, kc));
+}
+}  // namespace g4
+
+// one K-step of the wave's 128 x 64 tile: 8 A + 4 B fragment reads, 32 operand-swapped 16x16x32 MFMAs
+#define G4_STEP(CA, CB, FIRST)                                                                             \
+  {                                                                                                        \
+    e16x8 af[8], bf[4];                                                                                    \
+    _Pragma("unroll") for (int mi = 0; mi < 8; ++mi) af[mi] = g4::frag(CA, arow + mi * 16, kq);           \
+    _Pragma("unroll") for (int ni = 0; ni < 4; ++ni) bf[ni] = g4::frag(CB, brow + ni * 16, kq);           \
+    __builtin_amdgcn_s_setprio(1);                                                                         \
+    _Pragma("unroll") for (int mi = 0; mi < 8; ++mi)                                                       \
+    _Pragma("unroll") for (int ni = 0; ni < 4; ++ni)                                                       \
+      acc[mi][ni] = mma16(bf[ni], af[mi], (FIRST) ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);                  \
+    __builtin_amdgcn_s_setprio(0);                                                                         \
+  }
+
+template <int EPI, int FE>
+__global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  int bid = blockIdx.x;
+  {  // XCD-contiguous logical ids: the column tiles of one 256-row A panel share an L2
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = bid / per_batch, rem = bid - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 128;
+  const e16* A = (const e16*)p.A + bz * p.sA;
+  const e16* B = (const e16*)p.B + bz * p.sB;
+  const int nk = p.K / g4::KS;
+  const g4::Src src = g4::make_src(p, A, B, row0, col0, wave, lane);
+  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
+  f32x4 acc[8][4];
+
+  g4::stage(src, 0, gsm, wave);
+  if (nk > 1) g4::stage(src, g4::KS, gsm + g4::STAGE, wave);
+  // K-step t: stage t resident (stage t + 1 may stay in flight), every wave past step t - 1's fragment reads ->
+  // stage t + 2 refills the buffer of step t - 1
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (t + 2 < nk) g4::stage(src, (t + 2) * g4::KS, gsm + ((t + 2) % g4::NS) * g4::STAGE, wave);
+    const char* ca = gsm + (t % g4::NS) * g4::STAGE;
+    const char* cb = ca + g4::A_BYTES;
+    if (t == 0) G4_STEP(ca, cb, true) else G4_STEP(ca, cb, false)
+  }
+  if constexpr (FE == 1) {
+    ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+  } else {
+    ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+    ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
+  }
+}
+
+template <int EPI, int FE>
+int launch_gemm4w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + 127) / 128;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::LDS);
+    attr = true;
+  }
+  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
+  hipLaunchKernelGGL((gemm4w_kernel<EPI, FE>), dim3((unsigned)nwg), dim3(256), g4::LDS, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+// the lean kinds of the encoder's GEMMs (QKV / MLP1: e16 C; projections: fp32 C + in-place fp32 residual, with
+// or without the window row map) on the two-workgroup kernel: fast path 0 (default) when g_gemm4w, K % 32 == 0
+static int g_gemm4w = 1;
+template <int EPI>
+int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
+  switch (k.fast_epi) {
+    case 1: return launch_gemm4w_fe<EPI, 1>(k, a, s);
+    case 2: return launch_gemm4w_fe<EPI, 2>(k, a, s);
+    case 4: return launch_gemm4w_fe<EPI, 4>(k, a, s);
+    case 8: return launch_gemm4w_fe<EPI, 8>(k, a, s);
+    default: return -1;
+  }
 }
 
 // 256x192 tiles when they fill the chip's waves better than 256x256 ones (3/4 of the work per tile);
@@ -2141,6 +2274,7 @@ int& last_path() { static thread_local int v = 0; return v; }
 // disables the small-problem 64x64 path
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_small = (enable & 256) ? 0 : 1;
+  g_gemm4w = (enable & 512) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2252,6 +2386,14 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // fast path 11 forces the one-tile-per-workgroup kernel (A/B diagnostics)
       // (an e16 residual is allowed at small K: its loads drain the next tile's prefetch, which is the whole
       // next tile there anyway, and the tile's load latency still overlaps the epilogue)
+      // two workgroups per CU (gemm4w_kernel): the lean kinds without a broadcast residual, K % 32 == 0
+      if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->batch == 1 && am == 0 && bm == 0 &&
+          a->M >= 4096 && (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
+          (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 40)) {
+        t_last_path = 2;
+        if (a->act == OCTSAM_ACT_GELU) return launch_gemm4w<OCTSAM_ACT_GELU>(k, a, s);
+        return launch_gemm4w<0>(k, a, s);
+      }
       const bool res_small_k =
           a->R != nullptr && k.fast_epi == 11 && a->K <= 512 && a->act == 0;  // (kind 3 measured slower)
       // bias / activation kinds (encoder QKV, MLP1) run one tile per workgroup by default: under the encoder

@@ -690,13 +690,19 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
         # sum over steps of loss * images / global images on the device: no per-step host sync (the reference's
         # .item() of :69 only feeds this sum); one read per epoch
         loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
-        nxt = build(1, batches[1]) if len(batches) > 1 else None
+        # batches are built two ahead, in loader order (same RNG draws as building each at its own step): batch
+        # bi + 1 must exist when step bi is queued (its encoder runs during step bi's decoder), and batch bi + 2 is
+        # built on the host while the GPU runs step bi (forward_backward's `between`)
+        ready = {j: build(j, batches[j]) for j in (1, 2) if j < len(batches)}
         for bi, idx in enumerate(batches):
             if bi == 0:  # training_utils.py:40-44: the first batch of every epoch is skipped
                 continue
-            n_glob, batch, ev = nxt
-            # same batch order and RNG draws as building each batch at its own step (the builds stay in order)
-            nxt = build(bi + 1, batches[bi + 1]) if bi + 1 < len(batches) else None
+            n_glob, batch, ev = ready.pop(bi)
+            nxt = ready.get(bi + 1)
+
+            def ahead(j=bi + 2):
+                if j < len(batches):
+                    ready[j] = build(j, batches[j])
             if idx:
                 if ev is not None:
                     main.wait_event(ev)
@@ -707,10 +713,12 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
                     main.wait_event(nxt[2])
                 loss = step.forward_backward(*inputs_of(batch)[:2], input_boxes=batch.get("input_boxes"),
                                              input_points=batch.get("input_points"), crop=crop, orig=orig,
-                                             global_batch=n_glob, next_inputs=None if nb is None else inputs_of(nb))
+                                             global_batch=n_glob, next_inputs=None if nb is None else inputs_of(nb),
+                                             between=ahead)
                 loss_acc += loss[3:4].double() * len(idx) / n_glob
             else:  # nothing on this rank in a ragged last batch: contribute zero gradient
                 model.mask_decoder.flat_grad.zero_()
+                ahead()
             step._launch_update(len(idx), n_glob)  # all-reduce (overlapped with the next encoder forward) + Adam
         step.flush()
         epoch_loss = float(_collective_sum(loss_acc, pg)[0]) / len(batches)

@@ -90,7 +90,8 @@ int octsam_gemm(const octsam_gemm_args* args, void* stream);
 /* the same GEMM with IEEE-half 16-bit operands (A, B, and C / C_pre / R when not fp32): the fp16 encoder of
  * BASELINE configs[4] (sam-vit-huge, fp16) */
 int octsam_gemm_f16(const octsam_gemm_args* args, void* stream);
-/* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing) */
+/* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing);
+   bit 256 disables the small-problem tile kernel, bit 512 the two-workgroups-per-CU 256x128 kernel */
 void octsam_gemm_set_fast_path(int32_t enable);
 /* 1 if the calling thread's last octsam_gemm launched the persistent global_load_lds kernel
    (gemm_glds_kernel), 0 for the generic tile kernel. Used to attribute per-kernel timings. */
