@@ -2387,7 +2387,11 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // (an e16 residual is allowed at small K: its loads drain the next tile's prefetch, which is the whole
       // next tile there anyway, and the tile's load latency still overlaps the epilogue)
       // two workgroups per CU (gemm4w_kernel): the lean kinds without a broadcast residual, K % 32 == 0
-      if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->batch == 1 && am == 0 && bm == 0 &&
+      // (measured, scripts/gemm_ab.py, profiles/r03/gemm_ab.log: faster for N, K <= 1024 — proj 76 -> 69 us,
+      // decoder ConvT1 178 -> 173 us — and slower for the wide / deep ones: QKV 129 -> 140, MLP1 179 -> 194, MLP2
+      // 184 -> 195 us, where the 8-phase interleave of one 256x256 workgroup keeps the matrix pipes busier)
+      if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->K <= 1024 && a->N <= 1024 &&
+          a->batch == 1 && am == 0 && bm == 0 &&
           a->M >= 4096 && (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
           (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 40)) {
         t_last_path = 2;
