@@ -460,6 +460,113 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
   store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
+// ---------------------------------------------------------------- global, 4-wave workgroups (A/B variant 2)
+// The same per-lane arithmetic as vit_attn_global_kernel (bit-identical outputs) in 4-wave workgroups of 128
+// queries (two image rows) with a 2-deep K/V ring: 32 KiB of rel_h tables + 32 KiB (head_dim 80: 40) of ring per
+// workgroup, so two workgroups share a CU and each SIMD runs one wave of each. The 8-wave kernel's two waves on a
+// SIMD meet at the same per-tile barrier and run each phase (q.k on the matrix pipe, the exponentials on the
+// VALU, P.V) at the same time; waves of independent workgroups drift apart, so one's softmax issues beside the
+// other's products (PMC, profiles/r03/pmc/attn_global.summary.txt: VALU ~60 % and MFMA ~33 % busy, 40 % of wave
+// time waiting).
+constexpr int NW4 = 4, THR4 = NW4 * 64;
+constexpr int G4_RELH = NW4 * 64 * 32 * 4;  // rel_h tables [64 kh][32 q] fp32 per wave: 32 KiB
+template <int HD> constexpr int g4_smem() { return G4_RELH + 2 * Geo<HD>::TILE + 128; }
+static_assert(2 * g4_smem<80>() <= 160 * 1024, "two 4-wave global workgroups per CU");
+template <> __device__ __forceinline__ void wait_vm<16>() { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); }
+
+template <int HD, typename E>
+__global__ __launch_bounds__(THR4, 2) void vit_attn_global4_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+                                                                   const float* __restrict__ Rh,
+                                                                   const float* __restrict__ Rw, int heads, float scale) {
+  using G = Geo<HD>;
+  using V8 = typename ET<E>::v8;
+  constexpr int S = 64, T = 4096, NT = T / 64, QB = T / (NW4 * 32);  // 32 query blocks per (sequence, head)
+  static_assert(NW4 * G_SCR * 4 <= G4_RELH + 2 * G::TILE, "rel_w scratch must fit");
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            l32 = lane & 31;
+  const int lid = xcd_logical(blockIdx.x, gridDim.x);
+  const int qblk = lid % QB, head = (lid / QB) % heads, seq = (lid / QB) / heads;
+  const int D = heads * HD, ld = 3 * D;
+  const E* base = qkv + (long long)seq * T * ld;
+  const int q = qblk * (NW4 * 32) + wave * 32 + l32;
+  const int qh = q >> 6, qw = q & 63, qw0 = qw - l32;
+  const float c1 = scale * L2E;
+
+  V8 qf[G::NKS];
+  load_q<HD, E>(base + (long long)q * ld + head * HD, qf, h);
+  float* scr = (float*)gsm + wave * G_SCR;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const f32x16 t = rel_block<HD, E>(Rw, qw0 + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) scr[(32 * b + acc_row(r, h)) * 33 + l32] = t[r];
+  }
+  __syncthreads();
+  const float inv_scale = 1.0f / scale;
+  f32x16 relw[2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * 33 + l32] * inv_scale;
+  __syncthreads();
+  float* relh = (float*)gsm + wave * (64 * 32);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const f32x16 t = rel_block<HD, E>(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
+  }
+  char* ring = gsm + G4_RELH;
+  char* zero = ring + 2 * G::TILE;
+  if (tid < 32) ((float*)zero)[tid] = 0.0f;
+  __syncthreads();
+
+  const E* kbase = base + D + head * HD;
+  const E* vbase = base + 2 * D + head * HD;
+  load_tile<HD, NW4, E>(kbase, vbase, ld, 0, ring, wave, lane);
+
+  f32x16 acc_o[G::NTD];
+#pragma unroll
+  for (int td = 0; td < G::NTD; ++td) acc_o[td] = (f32x16)0.0f;
+  float m_run = -INFINITY, l_run = 0.0f;
+  for (int tile = 0; tile < NT; ++tile) {
+    // tile resident (the only load in flight); every wave is past tile - 1, whose slot takes tile + 1
+    wait_vm<0>();
+    raw_barrier();
+    if (tile + 1 < NT) load_tile<HD, NW4, E>(kbase, vbase, ld, (tile + 1) * 64, ring + ((tile + 1) & 1) * G::TILE, wave, lane);
+    const char* slot = ring + (tile & 1) * G::TILE;
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) sacc[t2] = qk_block<HD, E>(slot, t2, qf, relw[t2], l32, h);
+    const float rh = relh[tile * 32 + l32];
+    float mx = sacc[0][0];
+#pragma unroll
+    for (int i = 1; i < 31; i += 2) mx = max3f(mx, sacc[i >> 4][i & 15], sacc[(i + 1) >> 4][(i + 1) & 15]);
+    mx = fmaxf(mx, sacc[1][15]);
+    mx = max_halves(mx);
+    lazy_rescale<G::NTD>(fmaf(mx, c1, rh), m_run, l_run, acc_o);
+    const float c = rh - m_run;
+    f32x2 ls2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 x = {sacc[t2][r], sacc[t2][r + 1]};
+        const f32x2 y = x * c1 + c;  // v_pk_fma_f32
+        const f32x2 pv = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+        sacc[t2][r] = pv[0];
+        sacc[t2][r + 1] = pv[1];
+        ls2 += pv;  // v_pk_add_f32
+      }
+    l_run += ls2[0] + ls2[1];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) pv_step<HD, E>(slot, zero, ks, pack8<E>(sacc[ks >> 1], 8 * (ks & 1)), acc_o, lane);
+  }
+  const float l_tot = sum_halves(l_run);
+  store_out<HD, E>(out + ((long long)seq * T + q) * D + head * HD, acc_o, 1.0f / l_tot, h);
+}
+
 // ---------------------------------------------------------------- global, software-pipelined (A/B variant 0)
 // Same arithmetic as vit_attn_global_kernel (bit-identical outputs), reordered per wave so that its own
 // instruction stream keeps both pipes busy: the q.k MFMAs of tile t+1 issue while the VALU exponentiates tile t,
@@ -803,6 +910,15 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
         attr = true;
       }
       hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(), s,
+                         (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+    } else if (g_attn_variant == 2) {  // 4-wave workgroups, two per CU
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vit_attn_global4_kernel<HD, E>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, g4_smem<HD>());
+        attr = true;
+      }
+      hipLaunchKernelGGL((vit_attn_global4_kernel<HD, E>), dim3(32 * heads * nseq), dim3(THR4), g4_smem<HD>(), s,
                          (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
     } else {
       static bool attr = false;

@@ -86,7 +86,9 @@ class FusedTrainStep:
         # step t; 3 sets measured the same, 17.72 vs 17.76 ms/step: the encoder stream is busy throughout)
         self.pipeline_sets = 2
         self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
-        self._w2_stream = None  # side stream of the device W2 (forked from F2, joined before B)
+        self._w2_stream = None  # side stream of the device topological forward (forked in F2, joined before B)
+        # w2 = "device": the resampling + persistence run on that side stream too (False: in F, before the fork; A/B)
+        self.fork_topo = True
         self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
         self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
 
@@ -119,10 +121,14 @@ class FusedTrainStep:
         if self.topological and self.lamda != 0.0:
             entries, maps, midx = topo_index(B, N, self.topo_mode, st.global_batch, masks.device)
             if entries:
-                pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
                 st.topo_dev = (entries, maps, midx)
-                if self.w2 == "device":  # the transport runs in F2, beside the DiceCE backward
-                    st.w2_job = (pairs, cnt, vals, entries, maps, backward)
+                if self.w2 == "device" and self.fork_topo:
+                    # resampling, persistence and transport run in F2, beside the DiceCE backward
+                    st.w2_job = (entries, maps, midx, backward, None)
+                    return
+                pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
+                if self.w2 == "device":  # (fork_topo off, A/B: only the transport beside the DiceCE backward)
+                    st.w2_job = (entries, maps, midx, backward, (pairs, cnt, vals))
                 elif st.pinned is not None:  # graph mode: async copies into fixed pinned buffers
                     for h, d in zip(st.pinned, (pairs, cnt, vals)):
                         h.copy_(d, non_blocking=True)
@@ -130,22 +136,27 @@ class FusedTrainStep:
                     st.topo_out = (pairs, cnt, vals)
 
     def _phase_f2(self, st):
-        """DiceCE loss and its gradient, and (w2="device") beside it on a forked side stream the diagrams' W2
-        transport, topo loss and topo gradient (octsam_topo_w2: a few latency-bound workgroups, ~0.2 ms): the two
-        branches are independent and B joins them. w2="host": the host's W2 overlaps this phase instead (it waits on
-        an event between the graphs)."""
+        """DiceCE loss and its gradient, and (w2="device") beside it on a forked side stream the whole topological
+        forward: 50x50 resampling, persistence (one workgroup per map, ~0.55 ms), the diagrams' W2 transport, topo
+        loss and topo gradient (octsam_topo_w2) — a few latency-bound workgroups that the DiceCE kernels run beside;
+        B joins the two branches. w2="host": the persistence runs in F and the host's W2 overlaps this phase (it
+        waits on an event between the graphs)."""
         B, N, H, W = st.masks.shape
         job = getattr(st, "w2_job", None)
         if job is None:
             st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
             return
-        pairs, cnt, vals, entries, maps, want_grad = job
+        entries, maps, midx, want_grad, diagrams = job
         main = torch.cuda.current_stream()
         if self._w2_stream is None:
             self._w2_stream = torch.cuda.Stream(device=main.device)
         side = self._w2_stream
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            if diagrams is None:
+                pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
+            else:
+                pairs, cnt, vals = diagrams
             st.topo_loss_dev, st.dp = topo_w2_device(pairs, cnt, vals, entries, maps, lamda=self.lamda, feat_d=1,
                                                      loss_q=2, want_grad=want_grad)
         st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)

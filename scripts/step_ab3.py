@@ -1,7 +1,7 @@
 """Same-process A/B of the pipelined training step (bench.py's loop: hipGraphs + encoder lookahead, B = 8 boxes,
---top=True) for: the W2 transport on the device (default) vs on the host between the graphs (w2_host), and the
-per-step input copy-in on vs skipped (the same batch every step, so skipping changes no result). Interleaved
-rounds, median of 5 rounds x 20 steps. Diagnostic only."""
+--top=True) for: the topological forward (resampling, persistence, W2) forked beside the DiceCE backward (default),
+only the W2 forked (persistence in F), and the W2 on the host between the graphs (w2_host). Interleaved rounds,
+median of 5 rounds x 20 steps. Diagnostic only."""
 import json
 import os
 import statistics
@@ -23,11 +23,9 @@ def main():
         [sd[i] for i in range(8)]), "bboxes"), dev)
     model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(dev)
     variants = {}
-    for name, w2, copy in (("device", "device", True), ("w2_host", "host", True), ("device_nocopy", "device", False)):
+    for name, w2, fork in (("device", "device", True), ("device_ph_in_F", "device", False), ("w2_host", "host", True)):
         st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True, pipeline=True, w2=w2)
-        if not copy:
-            st._copy_in = lambda g, inputs: None
-            st._pixel_in = lambda es, px: None
+        st.fork_topo = fork
         variants[name] = st
     for st in variants.values():  # capture + warm
         for i in range(3):
