@@ -894,7 +894,10 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
   store_out<HD, E>(out + orow * D + head * HD, acc_o, 1.0f / l_tot, h);
 }
 
-int g_attn_variant = 1;  // 0: software-pipelined global kernel, 1 (default): the plain loop (octsam_attention_set_variant)
+// global-layer kernel (octsam_attention_set_variant): 0 software-pipelined 8-wave loop, 1 plain 8-wave loop, 2 4-wave
+// workgroups two per CU, -1 (default) 2 for head_dim 64 and 1 for head_dim 80 (same-box A/B, scripts/attn_ab.py,
+// profiles/r03/attn_variant_ab.log: vit-b 522.5 -> 498.6 us, vit-h fp16 929.6 vs 934.3 us; all bit-identical)
+int g_attn_variant = -1;
 
 template <int HD, typename E>
 int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nseq, int side, int heads, int grid,
@@ -902,7 +905,8 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
   const float scale = 1.0f / sqrtf((float)HD);
   if (side == 64) {
     static_assert(4096 / (NW * 32) == 16, "16 query blocks per (sequence, head)");
-    if (g_attn_variant == 1) {  // the plain loop (A/B)
+    const int variant = g_attn_variant >= 0 ? g_attn_variant : (HD == 64 ? 2 : 1);
+    if (variant == 1) {  // the plain loop (A/B)
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute((const void*)vit_attn_global_kernel<HD, E>,
@@ -911,7 +915,7 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
       }
       hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(), s,
                          (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
-    } else if (g_attn_variant == 2) {  // 4-wave workgroups, two per CU
+    } else if (variant == 2) {  // 4-wave workgroups, two per CU
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute((const void*)vit_attn_global4_kernel<HD, E>,

@@ -87,8 +87,11 @@ class FusedTrainStep:
         self.pipeline_sets = 2
         self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
         self._w2_stream = None  # side stream of the device topological forward (forked in F2, joined before B)
-        # w2 = "device": the resampling + persistence run on that side stream too (False: in F, before the fork; A/B)
-        self.fork_topo = True
+        # w2 = "device": only the transport forks beside the DiceCE backward, the resampling + persistence run in F
+        # (True: those forked too; same-process A/B, scripts/step_ab3.py, profiles/r03/step_ab_fork_tokdw.log:
+        # 17.04 vs 17.13 ms/step — the 16-workgroup persistence kernel beside the DiceCE backward delays it more
+        # than it gains)
+        self.fork_topo = False
         self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
         self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
 
@@ -127,7 +130,7 @@ class FusedTrainStep:
                     st.w2_job = (entries, maps, midx, backward, None)
                     return
                 pairs, cnt, vals = topo_device_forward(st.masks, st.gt_u8.view(B, N, H, W), midx, interp=self.interp)
-                if self.w2 == "device":  # (fork_topo off, A/B: only the transport beside the DiceCE backward)
+                if self.w2 == "device":  # (default: only the transport beside the DiceCE backward)
                     st.w2_job = (entries, maps, midx, backward, (pairs, cnt, vals))
                 elif st.pinned is not None:  # graph mode: async copies into fixed pinned buffers
                     for h, d in zip(st.pinned, (pairs, cnt, vals)):
@@ -136,10 +139,9 @@ class FusedTrainStep:
                     st.topo_out = (pairs, cnt, vals)
 
     def _phase_f2(self, st):
-        """DiceCE loss and its gradient, and (w2="device") beside it on a forked side stream the whole topological
-        forward: 50x50 resampling, persistence (one workgroup per map, ~0.55 ms), the diagrams' W2 transport, topo
-        loss and topo gradient (octsam_topo_w2) — a few latency-bound workgroups that the DiceCE kernels run beside;
-        B joins the two branches. w2="host": the persistence runs in F and the host's W2 overlaps this phase (it
+        """DiceCE loss and its gradient, and (w2="device") beside it on a forked side stream the diagrams' W2
+        transport, topo loss and topo gradient (octsam_topo_w2; with fork_topo also the 50x50 resampling and the
+        persistence) — a few latency-bound workgroups that the DiceCE kernels run beside; B joins the two branches. w2="host": the persistence runs in F and the host's W2 overlaps this phase (it
         waits on an event between the graphs)."""
         B, N, H, W = st.masks.shape
         job = getattr(st, "w2_job", None)

@@ -1,6 +1,7 @@
 """Same-process A/B of the pipelined training step (bench.py's loop: hipGraphs + encoder lookahead, B = 8 boxes,
 --top=True) for: the topological forward (resampling, persistence, W2) forked beside the DiceCE backward (default),
-only the W2 forked (persistence in F), and the W2 on the host between the graphs (w2_host). Interleaved rounds,
+only the W2 forked (persistence in F), the W2 on the host between the graphs (w2_host), and the token-side weight
+gradients as one GEMM each instead of split-K + reduction (device_tok_dw_1pass). Interleaved rounds,
 median of 5 rounds x 20 steps. Diagnostic only."""
 import json
 import os
@@ -23,14 +24,17 @@ def main():
         [sd[i] for i in range(8)]), "bboxes"), dev)
     model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(dev)
     variants = {}
-    for name, w2, fork in (("device", "device", True), ("device_ph_in_F", "device", False), ("w2_host", "host", True)):
+    dec = model.mask_decoder
+    for name, w2, fork, tok_split in (("device", "device", True, True), ("device_ph_in_F", "device", False, True),
+                                      ("w2_host", "host", True, True), ("device_tok_dw_1pass", "device", True, False)):
         st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True, pipeline=True, w2=w2)
         st.fork_topo = fork
-        variants[name] = st
-    for st in variants.values():  # capture + warm
-        for i in range(3):
+        dec.token_dw_split = tok_split  # read while the graphs are captured
+        for i in range(3):  # capture + warm
             st.step(batch, next_batch=batch if i < 2 else None)
         st.flush()
+        dec.token_dw_split = True
+        variants[name] = st
     torch.cuda.synchronize()
     res = {k: [] for k in variants}
     n = 20

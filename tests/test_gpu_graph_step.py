@@ -35,6 +35,29 @@ def test_graph_step_matches_eager(cuda, top):
         assert float(lg[-1][2]) > 0.0
 
 
+@pytest.mark.parametrize("variant", ["fork_topo", "w2_host"])
+def test_graph_step_topo_variants_match_default(cuda, variant):
+    """The A/B arrangements of the topological forward inside the graphs — resampling + persistence forked beside the
+    DiceCE backward too (fork_topo), the transport on the host between F and B (w2="host") — give the same losses and
+    updated weights as the default graph step (the same kernels; host W2 is bit-identical to the device one)."""
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    batch = _batch(cuda)
+    runs = []
+    for v in ("default", variant):
+        model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(cuda)
+        step = FusedTrainStep(model, topological=True, graphs=True, w2="host" if v == "w2_host" else "device")
+        step.fork_topo = v == "fork_topo"
+        losses = [step.step(batch).clone() for _ in range(3)]
+        step.flush()
+        torch.cuda.synchronize()
+        runs.append((losses, model.mask_decoder.flat.detach().clone()))
+    (la, fa), (lb, fb) = runs
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b), (a, b)
+    assert torch.equal(fa, fb)
+
+
 def test_graph_step_new_batches_match_eager(cuda):
     """Graph mode with a new batch every step (the end-to-end bench loop): one capture per batch shape, later
     batches of a captured shape copied into the static inputs; host prompts (the device data path's output)
