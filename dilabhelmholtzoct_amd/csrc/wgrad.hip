@@ -1,0 +1,282 @@
+// Image-side weight gradients of the mask decoder (the backward of the per-prompt image-side projections,
+// hf modeling_sam.py:219-221 / 254 q,k,v_proj and out_proj on the keys, and the upscaling ConvT1 :1054):
+//
+//   out[o][i] (+)= sum_m dY[m][o] * X[m][i]      m over the P*4096 per-prompt image rows (688 128 at the bench)
+//   db[o] = sum_m dY[m][o],  dbx[i mod I/fold] = sum_m X[m][i]            (bias gradients, optional)
+//
+// with O in {128, 256, 384} and I in {128, 256}: a tall reduction whose operands (O + I bf16 per row, 1280 B at
+// O = 384, I = 256) are the whole cost. Each workgroup holds the WHOLE O x I output in its accumulators (8 waves as
+// 2 (O) x 4 (I), up to 192 fp32 per lane) and streams one contiguous range of rows through a 4-stage LDS-DMA ring,
+// so every operand byte crosses HBM once and 80-120 KB per CU stay in flight. (The split-K tile GEMM it replaces
+// re-reads A per N tile and B per M tile through L2, keeps one 48 KB stage in flight and reached 1.85 TB/s,
+// scripts/dw_ab.py.) Fragments come from the LDS images by ds_read_b64_tr_b16 (the operands are k-major: row m of
+// dY holds the k-th element of every output row o). The per-workgroup partials (fp32 [nwg][O][I], plus the column
+// sums) are summed over workgroups in a fixed order by a second launch: deterministic, independent of timing.
+#include "common.h"
+#include "../../include/octsam.h"
+
+extern "C" int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta,
+                                    void* stream);
+
+namespace {
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int SROWS = 32;  // rows (k) per ring stage
+constexpr int NS = 4;      // ring stages (160 KB at O = 384, I = 256)
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Stage image of a k-major operand [SROWS rows][W columns] in 8-row x 32-column subtiles of 512 B (64-B rows), laid
+// out across the whole width so that subtile X of a row group sits at a constant 512 X: byte offset of 16-B chunk
+// ch of row r = rowg (r >> 3) + 512 (ch >> 2) + 64 (r & 7) + 16 (ch & 3), rowg = 16 W. A fragment read (32 lanes:
+// 4 rows x 2 x 16 columns) then covers 4 whole 64-B rows = all 64 banks once: conflict-free without a swizzle, and
+// the second read of a fragment (rows + 4) is the first one + 256 B.
+//
+// One stage: 1 KiB LDS-DMA buffer loads, each two subtiles (64 columns) of one row group; instruction J of the
+// W/64 per row group, wave w issues J = w, w + 8, ... (J counted across both operands: j0 = the instructions of the
+// operand before this one). The buffer descriptor spans the workgroup's rows only, so rows past its range read as
+// zero through the hardware range check. voffset = the lane's part (row rr of the group, chunk 4 st + slot: the
+// same for every instruction); soffset = the wave-uniform rest (16 ld gq + 128 jp + the stage's rows).
+__device__ __forceinline__ int stage_lane_off(long long ld, int lane) {
+  const int st = lane >> 5, rr = (lane >> 2) & 7, slot = lane & 3;
+  return (int)(rr * ld * 2) + 64 * st + 16 * slot;
+}
+template <int W, int NJ>
+__device__ __forceinline__ void stage_load(const bf16* base, int bytes, long long ld, int soff, char* lds, int voff,
+                                           int wave, int j0) {
+  constexpr int PER_G = W / 64, NINST = 4 * PER_G, ROWG = 16 * W;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int J = wave + 8 * jj - j0;  // wave-uniform
+    if (J >= 0 && J < NINST) {
+      const int gq = J / PER_G, jp = J - gq * PER_G;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(lds + ROWG * gq + 1024 * jp), 16, voff,
+                                               soff + (int)(16 * ld * gq) + 128 * jp, 0, 0);
+    }
+  }
+}
+
+// lane part of a fragment read address (32x32x16 operand: 8 consecutive k, k = kb + 8 (lane >> 5) + t, of column
+// 32 X + (lane & 31)): lane 4q + p of each 16-lane group gives row 8 (g >> 1) + q, columns 4p .. 4p + 3 of its
+// 16-column block (chunk 2 (g & 1) + (p >> 1)); the subtile (512 X), the k block (rowg kb / 8) and the second read
+// (+256: rows + 4) are immediates
+template <int W>
+__device__ __forceinline__ int frag_lane_off(int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  return 16 * W * (g >> 1) + 64 * q + 16 * (2 * (g & 1) + (p >> 1)) + 8 * (p & 1);
+}
+
+__device__ __forceinline__ bf16x8 frag(const char* base, int imm) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + imm));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + imm + 256));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// s + the 8 elements of a fragment (v_dot2 with ones: exact products, fp32 sums, fixed order)
+__device__ __forceinline__ float frag_sum(bf16x8 v, float s) {
+  const bf16x2 one = {(bf16)1.0f, (bf16)1.0f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bf16x2 pr = {v[2 * q], v[2 * q + 1]};
+    s = __builtin_amdgcn_fdot2_f32_bf16(pr, one, s, false);
+  }
+  return s;
+}
+
+template <int GLW>
+__device__ __forceinline__ void wait_stage(int ahead) {  // leave `ahead` younger stages (GLW loads each) in flight
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GLW) : "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GLW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// NBO x NBI 32x32 accumulator blocks per wave: O = 64 NBO (2 wave rows), I = 128 NBI (4 wave columns)
+template <int NBO, int NBI>
+__global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ dy, long long ldy,
+                                                       const bf16* __restrict__ x, long long ldx, long long M,
+                                                       long long rows_per, float* __restrict__ part,
+                                                       float* __restrict__ cs_a, float* __restrict__ cs_b) {
+  constexpr int O = 64 * NBO, I = 128 * NBI;
+  constexpr int A_BYTES = SROWS * O * 2, STAGE = SROWS * (O + I) * 2;
+  constexpr int NA = O / 16, NB = I / 16, GLW = (NA + NB) / 8;  // 1 KiB loads per stage: per operand, per wave
+  static_assert(NBO % 2 == 0 && (NA + NB) % 8 == 0 && NS * STAGE <= 160 * 1024, "stage ring exceeds the LDS");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave >> 2, wi = wave & 3;
+  const long long m_beg = (long long)blockIdx.x * rows_per;
+  const long long m_end = min(M, m_beg + rows_per);
+  const int nst = (int)((m_end - m_beg + SROWS - 1) / SROWS);  // >= 1 (host sizes the grid)
+
+  // instructions per wave: A covers J in [0, NA), B in [NA, NA + NB)
+  constexpr int NJA = (NA + 7) / 8, NJB = (NA + NB + 7) / 8;
+  int va = stage_lane_off(ldy, lane), vb = stage_lane_off(ldx, lane);
+  asm volatile("" : "+v"(va), "+v"(vb));
+  const bf16* a_base = dy + m_beg * ldy;
+  const bf16* b_base = x + m_beg * ldx;
+  const int a_bytes = (int)((m_end - m_beg) * ldy * 2), b_bytes = (int)((m_end - m_beg) * ldx * 2);
+  auto issue = [&](int s) {
+    char* st = smem + (s % NS) * STAGE;
+    stage_load<O, NJA>(a_base, a_bytes, ldy, (int)(s * SROWS * ldy * 2), st, va, wave, 0);
+    stage_load<I, NJB>(b_base, b_bytes, ldx, (int)(s * SROWS * ldx * 2), st + A_BYTES, vb, wave, NA);
+  };
+  // fragment bases: lane part + this wave's first subtile (A: 32 NBO wo columns, B: 32 NBI wi columns)
+  int a_off = frag_lane_off<O>(lane) + 512 * NBO * wo;
+  int b_off = A_BYTES + frag_lane_off<I>(lane) + 512 * NBI * wi;
+  // one register each: keep the compiler from carrying the sums' terms separately (the accumulators leave few)
+  asm volatile("" : "+v"(a_off), "+v"(b_off));
+
+  f32x16 acc[NBO][NBI];
+#pragma unroll
+  for (int b = 0; b < NBO; ++b)
+#pragma unroll
+    for (int c = 0; c < NBI; ++c) acc[b][c] = (f32x16)0.0f;
+  // column sums: A block b of wave row wo is summed by the wave with wi == b % 4 (into csa[b / 4]), B block c of
+  // wave column wi by the wave with wo == c: every column exactly once per workgroup
+  float csa[(NBO + 3) / 4], csb = 0.0f;
+#pragma unroll
+  for (int b = 0; b < (NBO + 3) / 4; ++b) csa[b] = 0.0f;
+  const bool want_a = cs_a != nullptr, want_b = cs_b != nullptr && wo < NBI;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nst) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    wait_stage<GLW>(min(NS - 2, nst - 1 - s));
+    raw_barrier();
+    if (s + NS - 1 < nst) issue(s + NS - 1);
+    const char* sg = smem + (s % NS) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < SROWS / 16; ++kk) {
+      bf16x8 bfr[NBI];
+#pragma unroll
+      for (int c = 0; c < NBI; ++c) bfr[c] = frag(sg + b_off, 32 * I * kk + 512 * c);
+#pragma unroll
+      for (int b = 0; b < NBO; ++b) {
+        const bf16x8 af = frag(sg + a_off, 32 * O * kk + 512 * b);
+#pragma unroll
+        for (int c = 0; c < NBI; ++c)
+          acc[b][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[c], acc[b][c], 0, 0, 0);
+        if (want_a && (b & 3) == wi) csa[b >> 2] = frag_sum(af, csa[b >> 2]);
+      }
+      if (want_b) {
+        bf16x8 f = bfr[0];
+#pragma unroll
+        for (int c = 1; c < NBI; ++c) f = wo == c ? bfr[c] : f;
+        csb = frag_sum(f, csb);
+      }
+    }
+  }
+
+  // partials: element e of block (b, c) is out[o][i], o = ob + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), i = ib + lane & 31
+  // (buffer stores: one lane offset for every element, the element's row and block offsets are wave-uniform)
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(part + (long long)blockIdx.x * O * I), (short)0, O * I * 4, 0x00020000);
+  const int p_lane = ((wo * 32 * NBO + 4 * (lane >> 5)) * I + wi * 32 * NBI + (lane & 31)) * 4;
+#pragma unroll
+  for (int b = 0; b < NBO; ++b)
+#pragma unroll
+    for (int c = 0; c < NBI; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        // (copy the element out first: a bit_cast of the vector-element lvalue reads element 0)
+        const float v = acc[b][c][e];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rp, p_lane,
+                                              ((32 * b + (e & 3) + 8 * (e >> 2)) * I + 32 * c) * 4, 0);
+      }
+  if (want_a) {
+#pragma unroll
+    for (int b = 0; b < NBO; ++b)
+      if ((b & 3) == wi) {  // lanes l and l + 32 hold the two k halves of column (l & 31)
+        const float v = csa[b >> 2] + __shfl_xor(csa[b >> 2], 32, 64);
+        if (lane < 32) cs_a[(long long)blockIdx.x * O + wo * 32 * NBO + 32 * b + lane] = v;
+      }
+  }
+  if (want_b) {
+    const float v = csb + __shfl_xor(csb, 32, 64);
+    if (lane < 32) cs_b[(long long)blockIdx.x * I + wi * 32 * NBI + 32 * wo + lane] = v;
+  }
+}
+
+int n_workgroups(long long M, long long& rows_per) {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+  }
+  rows_per = SROWS * ((M + (long long)SROWS * n_cu - 1) / ((long long)SROWS * n_cu));
+  return (int)((M + rows_per - 1) / rows_per);
+}
+
+template <int NBO, int NBI>
+int launch(const bf16* dy, long long ldy, const bf16* x, long long ldx, long long M, long long rows_per, int nwg,
+           float* part, float* cs_a, float* cs_b, hipStream_t s) {
+  constexpr int STAGE = SROWS * (64 * NBO + 128 * NBI) * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_kernel<NBO, NBI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              NS * STAGE);
+    attr = true;
+  }
+  hipLaunchKernelGGL((wgrad_kernel<NBO, NBI>), dim3(nwg), dim3(512), NS * STAGE, s, dy, ldy, x, ldx, M, rows_per,
+                     part, cs_a, cs_b);
+  OCTSAM_LAUNCH_CHECK("octsam_wgrad");
+  return 0;
+}
+}  // namespace
+
+extern "C" int32_t octsam_wgrad_supported(int64_t M, int32_t O, int32_t I) {
+  return M > 0 && (O == 128 || O == 256 || O == 384) && (I == 128 || I == 256) ? 1 : 0;
+}
+
+extern "C" int64_t octsam_wgrad_workspace(int64_t M, int32_t O, int32_t I) {
+  if (!octsam_wgrad_supported(M, O, I)) return 0;
+  long long rows_per;
+  const int nwg = n_workgroups(M, rows_per);
+  return (int64_t)nwg * ((int64_t)O * I + O + I) * 4;
+}
+
+extern "C" int octsam_wgrad(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I,
+                            float* out, float beta, float* db, float* dbx, int32_t dbx_fold, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  OCTSAM_CHECK_ARG(octsam_wgrad_supported(M, O, I), "octsam_wgrad: unsupported shape M=%lld O=%d I=%d "
+                   "(O in {128, 256, 384}, I in {128, 256})", (long long)M, O, I);
+  OCTSAM_CHECK_ARG(dy && x && out && workspace, "octsam_wgrad: null pointer");
+  OCTSAM_CHECK_ARG(ldy >= O && ldx >= I && ldy % 8 == 0 && ldx % 8 == 0,
+                   "octsam_wgrad: ldy=%lld / ldx=%lld must be >= O / I and multiples of 8", (long long)ldy,
+                   (long long)ldx);
+  OCTSAM_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)workspace & 15) == 0,
+                   "octsam_wgrad: operands and workspace must be 16-B aligned");
+  OCTSAM_CHECK_ARG(dbx == nullptr || (dbx_fold >= 1 && I % dbx_fold == 0 && (I / dbx_fold) % 4 == 0),
+                   "octsam_wgrad: dbx_fold=%d must divide I=%d into a multiple of 4 columns", dbx_fold, I);
+  OCTSAM_CHECK_ARG(workspace_bytes >= octsam_wgrad_workspace(M, O, I), "octsam_wgrad: workspace too small");
+  long long rows_per;
+  const int nwg = n_workgroups(M, rows_per);
+  float* part = (float*)workspace;
+  float* cs_a = db ? part + (long long)nwg * O * I : nullptr;
+  float* cs_b = dbx ? part + (long long)nwg * (O * I + O) : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16 *A = (const bf16*)dy, *B = (const bf16*)x;
+  int rc;
+  if (O == 384 && I == 256) rc = launch<6, 2>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  else if (O == 384) rc = launch<6, 1>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  else if (O == 256 && I == 256) rc = launch<4, 2>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  else if (O == 256) rc = launch<4, 1>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  else if (I == 256) rc = launch<2, 2>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  else rc = launch<2, 1>(A, ldy, B, ldx, M, rows_per, nwg, part, cs_a, cs_b, s);
+  if (rc) return rc;
+  if ((rc = octsam_splitk_reduce(part, out, (int64_t)O * I, nwg, beta, stream))) return rc;
+  if (db && (rc = octsam_splitk_reduce(cs_a, db, O, nwg, 0.0f, stream))) return rc;
+  if (dbx && (rc = octsam_splitk_reduce(cs_b, dbx, I / dbx_fold, nwg * dbx_fold, 0.0f, stream))) return rc;
+  return 0;
+}

@@ -268,6 +268,10 @@ class MaskDecoder(nn.Module):
         K.gemm(src_b, w, M=M, N=N, K=C, out=out, residual=P, ldr=N, r_remap=(L_IMG, max(1, M // L_IMG)), ldc=N)
         return out
 
+    # image-side weight gradients through octsam_wgrad (False: the split-K tile GEMM + reduction; A/B,
+    # scripts/dw_ab.py / scripts/step_ab3.py)
+    wide_wgrad = True
+
     @staticmethod
     def _pick_split(Mtok, O, I):
         """Split-K (splits, rows per split) for a weight gradient with Mtok reduction rows: enough (O x I tiles)
@@ -310,11 +314,16 @@ class MaskDecoder(nn.Module):
             self._dw(dy, x, M, out, ldy=ldy, ldx=ldx, accumulate=accumulate, db=db, dbx=dbx, dbx_fold=dbx_fold)
             self._dw(S, x_add, rows, out, ldy=O, ldx=ldx, accumulate=True)
             return out
+        beta = 1.0 if accumulate else 0.0
+        if (split is None and self.wide_wgrad and M >= 65536 and K.wgrad_supported(M, O, I) and ldy % 8 == 0
+                and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0):
+            # image side: one workgroup per CU holds the whole O x I output and streams its rows (octsam_wgrad)
+            K.wgrad(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db, dbx=dbx, dbx_fold=dbx_fold)
+            return out
         if split is None:
             split, Ks = self._pick_split(M, O, I)
         else:
             Ks = M // split
-        beta = 1.0 if accumulate else 0.0
         dev = out.device
         pa = torch.empty((split, O), device=dev, dtype=torch.float32) if db is not None else None
         pb = torch.empty((split, I), device=dev, dtype=torch.float32) if dbx is not None else None

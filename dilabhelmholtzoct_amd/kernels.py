@@ -91,6 +91,32 @@ def splitk_reduce(partials: torch.Tensor, out: torch.Tensor, splits: int, beta: 
     return out
 
 
+def wgrad_supported(M: int, O: int, I: int) -> bool:
+    return bool(_lib.load().octsam_wgrad_supported(M, O, I))
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, M: int, out: torch.Tensor, *, ldy: int | None = None,
+          ldx: int | None = None, beta: float = 0.0, db: torch.Tensor | None = None, dbx: torch.Tensor | None = None,
+          dbx_fold: int = 1) -> torch.Tensor:
+    """out[O, I] = beta * out + dy[M, O]^T x[M, I] (bf16 operands with row strides ldy / ldx, fp32 out), db = column
+    sums of dy, dbx = column sums of x folded over dbx_fold column groups (octsam_wgrad)."""
+    _require_cuda(dy, x, out, db, dbx)
+    O, I = out.shape
+    ldy = O if ldy is None else ldy
+    ldx = I if ldx is None else ldx
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32:
+        raise ValueError("wgrad: bf16 operands and an fp32 output")
+    for name, t in (("db", db), ("dbx", dbx)):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError(f"wgrad: {name} must be contiguous fp32")
+    lib = _lib.load()
+    nbytes = lib.octsam_wgrad_workspace(M, O, I)
+    ws = torch.empty(max(nbytes, 16), device=out.device, dtype=torch.uint8)
+    _lib.call("octsam_wgrad", ptr(dy), ldy, ptr(x), ldx, M, O, I, ptr(out), beta, ptr(db), ptr(dbx), dbx_fold,
+              ptr(ws), nbytes)
+    return out
+
+
 def ph_max_pairs(H: int, W: int) -> int:
     """Pair-buffer length that no [H, W] map can overflow: finite H0 pairs are born at regional minima
     (pairwise non-8-adjacent, <= ceil(H/2)*ceil(W/2)) and H1 pairs die at regional maxima (pairwise

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 13
+#define OCTSAM_ABI_VERSION 14
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -100,6 +100,21 @@ int32_t octsam_gemm_last_path(void);
 /* out[i] = sum_{s<splits} partials[s*n+i] + beta*out[i]  (fp32; deterministic split-K combine) */
 int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta, void* stream);
 
+/* Image-side weight gradient of the mask decoder (replaces the per-prompt image-side projections' and the ConvT1
+ * weight-gradient GEMMs of the reference's autograd backward, hf modeling_sam.py:219-221/254 k/q/v/out_proj on the
+ * keys and :1054 upscale_conv1 — dW = dY^T X over the P*4096 image rows):
+ *   out[o][i] = beta*out[o][i] + sum_m dy[m*ldy + o] * x[m*ldx + i]              (bf16 operands, fp32 out)
+ *   db[o] = sum_m dy[m*ldy + o];  dbx[c] = sum_m sum_t x[m*ldx + t*(I/dbx_fold) + c]   (optional, overwrite)
+ * O in {128, 256, 384}, I in {128, 256} (octsam_wgrad_supported); ldy, ldx multiples of 8, dy / x / workspace
+ * 16-B aligned. One workgroup per CU holds the whole O x I output and streams a contiguous row range (each operand
+ * byte read once); per-workgroup partials are combined in fixed order (deterministic).
+ * workspace: octsam_wgrad_workspace(M, O, I) bytes. */
+int32_t octsam_wgrad_supported(int64_t M, int32_t O, int32_t I);
+int64_t octsam_wgrad_workspace(int64_t M, int32_t O, int32_t I);
+int octsam_wgrad(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I, float* out,
+                 float beta, float* db, float* dbx, int32_t dbx_fold, void* workspace, int64_t workspace_bytes,
+                 void* stream);
+
 /* ---------------------------------------------------------------- cubical persistence
  * Replaces torch_topological.nn.CubicalComplex(dim=2, superlevel=False)._forward ->
  * gudhi.CubicalComplex(dimensions=x.shape, top_dimensional_cells=x.flatten()).persistence()
@@ -152,8 +167,10 @@ int octsam_layernorm_bwd(const void* dy, int32_t dy_f32, const void* x, int32_t 
 int octsam_vit_attention(const void* qkv, void* out, const float* rel_pos_h, const float* rel_pos_w, int32_t nseq,
                          int32_t side, int32_t heads, int32_t head_dim, int32_t fp16, int32_t grid,
                          const void* pad_row, void* stream);
-/* A/B switch for the global layers' kernel: 1 (default) = the plain per-tile loop, 0 = software-pipelined (q.k of
-   the next key tile beside the softmax of this one: bit-identical, measured no faster, profiles/r03/attn_pipelined_ab.log) */
+/* A/B switch for the global layers' kernel (all bit-identical): -1 (default) = 2 for head_dim 64, 1 for head_dim 80;
+   1 = the plain per-tile loop of 8-wave workgroups; 2 = 4-wave workgroups, two per CU (vit-b 522.5 -> 498.6 us,
+   profiles/r03/attn_variant_ab.log); 0 = software-pipelined (q.k of the next key tile beside the softmax of this one:
+   measured no faster, profiles/r03/attn_pipelined_ab.log) */
 void octsam_attention_set_variant(int32_t variant);
 
 /* ---------------------------------------------------------------- element-wise / reductions / prompts */

@@ -528,3 +528,45 @@ def test_cast_vectorized(cuda, n):
             out = torch.empty(n, device=cuda, dtype=dt)
             kernels.cast_bf16(src, out)
             assert torch.equal(out, src.to(dt))
+
+
+@pytest.mark.parametrize("M,O,I,ldy_pad,ldx_pad,db,fold,beta", [
+    (688128, 384, 256, 0, 0, True, 0, 0.0),    # the bench's K|Q'|V dW (P = 168 prompts)
+    (70000, 384, 128, 8, 0, True, 1, 0.0),     # ragged rows (not a multiple of 32 x workgroups), strided dY
+    (65536, 256, 256, 0, 128, False, 4, 0.0),  # ConvT1: bias of x folded over 4 taps, strided X
+    (100003, 256, 128, 0, 0, True, 0, 1.0),    # accumulate into out
+    (66000, 128, 256, 0, 0, False, 0, 0.0),
+    (2000, 128, 128, 0, 0, True, 2, 0.0),      # fewer rows than workgroups x 32
+])
+def test_wgrad(cuda, M, O, I, ldy_pad, ldx_pad, db, fold, beta):
+    """octsam_wgrad (image-side dW = dY^T X, whole output per workgroup) vs torch fp32 on the same bf16 operands,
+    with the fused bias column sums; fixed-order combine: bitwise repeatable."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(M + O + I)
+    ldy, ldx = O + ldy_pad, I + ldx_pad
+    dy = torch.randn(M, ldy, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ldx, generator=g).to(cuda, torch.bfloat16)
+    out0 = torch.randn(O, I, generator=g).to(cuda)
+    out = out0.clone()
+    gdb = torch.empty(O, device=cuda) if db else None
+    gdbx = torch.empty(I // max(fold, 1), device=cuda) if fold else None
+    kernels.wgrad(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=gdb, dbx=gdbx, dbx_fold=max(fold, 1))
+    ref = dy[:, :O].float().t() @ x[:, :I].float() + beta * out0
+    assert _rel(out, ref) < 1e-5
+    if db:
+        assert _rel(gdb, dy[:, :O].float().sum(0)) < 1e-5
+    if fold:
+        assert _rel(gdbx, x[:, :I].float().sum(0).view(fold, -1).sum(0)) < 1e-5
+    again = out0.clone()
+    kernels.wgrad(dy, x, M, again, ldy=ldy, ldx=ldx, beta=beta, db=None, dbx=None)
+    assert torch.equal(again, out)
+
+
+def test_wgrad_rejects_unsupported(cuda):
+    from dilabhelmholtzoct_amd import kernels
+    from dilabhelmholtzoct_amd._lib import OctsamError
+    assert not kernels.wgrad_supported(1000, 192, 256)
+    dy = torch.zeros(1000, 192, device=cuda, dtype=torch.bfloat16)
+    x = torch.zeros(1000, 256, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(OctsamError):
+        kernels.wgrad(dy, x, 1000, torch.empty(192, 256, device=cuda))
