@@ -50,6 +50,8 @@ _SIGNATURES = {
     "octsam_gemm_last_path": (c_int32, []),
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
     "octsam_wgrad_supported": (c_int32, [c_int64, c_int32, c_int32]),
+    "octsam_wgrad_tok": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_float,
+                                   c_void_p, c_void_p]),
     "octsam_wgrad_workspace": (c_int64, [c_int64, c_int32, c_int32]),
     "octsam_wgrad": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_float,
                                c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),

@@ -41,9 +41,10 @@ __device__ __forceinline__ void raw_barrier() {
 //
 // One stage: 1 KiB LDS-DMA buffer loads, each two subtiles (64 columns) of one row group; instruction J of the
 // W/64 per row group, wave w issues J = w, w + 8, ... (J counted across both operands: j0 = the instructions of the
-// operand before this one). The buffer descriptor spans the workgroup's rows only, so rows past its range read as
-// zero through the hardware range check. voffset = the lane's part (row rr of the group, chunk 4 st + slot: the
-// same for every instruction); soffset = the wave-uniform rest (16 ld gq + 128 jp + the stage's rows).
+// operand before this one). The buffer descriptor spans the workgroup's rows only; voffset = the lane's part (row rr
+// of the group, chunk 4 st + slot: the same for every instruction), soffset = the stage's rows + 16 ld gq + 128 jp.
+// Rows past the range read as zero: gfx950's raw-buffer range check covers voffset + soffset (measured,
+// scripts/probe/range_probe.hip), so a workgroup's partial last stage needs no per-lane test.
 __device__ __forceinline__ int stage_lane_off(long long ld, int lane) {
   const int st = lane >> 5, rr = (lane >> 2) & 7, slot = lane & 3;
   return (int)(rr * ld * 2) + 64 * st + 16 * slot;
@@ -206,6 +207,108 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Token-side weight gradients (the P*T prompt-token rows, a few thousand: the decoder's token projections, MLPs and
+// hypernetworks): out[o][i] (+)= sum_m dY[m][o] X[m][i] and db[o] = sum_m dY[m][o] in ONE launch. Workgroup = one
+// 32 x 32 output tile; its NW waves split the rows into NW contiguous ranges and each streams its range through a
+// wave-private 4-stage LDS-DMA ring (32 rows x 32 columns of each operand per stage, no workgroup barrier in the
+// loop), one 32x32x16 MFMA per 16 rows; the NW partial tiles (and column sums) are added in fixed wave order
+// through LDS. Replaces the split-K tile GEMM + its reduction + the bias column-sum kernel + its reduction.
+namespace tok {
+constexpr int NST = 4;                    // ring stages per wave
+constexpr int OPB = SROWS * 32 * 2;       // bytes of one operand per stage (2 KiB)
+constexpr int STB = 2 * OPB;              // stage bytes (A then B)
+
+// one operand's stage: two 1 KiB loads (rows 0-15, 16-31), lane -> (row group l >> 5, row (l >> 2) & 7, chunk l & 3)
+__device__ __forceinline__ void tok_load(__amdgpu_buffer_rsrc_t rs, int voff, int soff, long long ld, char* lds) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(lds + 1024 * h), 16, voff, soff + (int)(32 * ld * h), 0,
+                                             0);
+}
+}  // namespace tok
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restrict__ dy, long long ldy,
+                                                            const bf16* __restrict__ x, long long ldx, long long M,
+                                                            int tiles_i, float* __restrict__ out, int ldo, float beta,
+                                                            float* __restrict__ db) {
+  using namespace tok;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int to = blockIdx.x / tiles_i, ti = blockIdx.x - to * tiles_i;
+  const int o0 = to * 32, i0 = ti * 32;
+  // this wave's rows: [m_beg, m_end), 32-row multiples except the last range
+  const long long per = ((M + NW - 1) / NW + SROWS - 1) / SROWS * SROWS;
+  const long long m_beg = min(M, (long long)wave * per), m_end = min(M, m_beg + per);
+  const int nst = (int)((m_end - m_beg + SROWS - 1) / SROWS);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dy + m_beg * ldy + o0), (short)0, (int)((m_end - m_beg) * ldy * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + m_beg * ldx + i0), (short)0, (int)((m_end - m_beg) * ldx * 2), 0x00020000);
+  const int rr = 8 * (lane >> 5) + ((lane >> 2) & 7), slot = lane & 3;
+  int va = (int)(rr * ldy * 2) + 16 * slot, vb = (int)(rr * ldx * 2) + 16 * slot;
+  char* ring = smem + wave * NST * STB;
+  // fragment read: 32 x 32 image (one subtile column), lane part as frag_lane_off<32>
+  const int fo = frag_lane_off<32>(lane);
+
+  f32x16 acc = (f32x16)0.0f;
+  float cs = 0.0f;
+  const bool want_cs = db != nullptr && ti == 0;
+  auto issue = [&](int s) {
+    char* st = ring + (s % NST) * STB;
+    tok::tok_load(ra, va, (int)(s * SROWS * ldy * 2), ldy, st);
+    tok::tok_load(rb, vb, (int)(s * SROWS * ldx * 2), ldx, st + OPB);
+  };
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nst) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    if (s + NST - 1 < nst) {
+      issue(s + NST - 1);  // (its slot's reads finished in iteration s - 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NST - 1)) : "memory");
+    } else {
+      const int ahead = nst - 1 - s;  // 0 .. NST-2 younger stages
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* sg = ring + (s % NST) * STB + fo;
+#pragma unroll
+    for (int kk = 0; kk < SROWS / 16; ++kk) {
+      const bf16x8 af = frag(sg, 1024 * kk);
+      const bf16x8 bfr = frag(sg + OPB, 1024 * kk);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc, 0, 0, 0);
+      if (want_cs) cs = frag_sum(af, cs);
+    }
+  }
+  // fixed-order sum of the NW partial tiles (and column sums) through LDS (the rings are no longer read)
+  __syncthreads();
+  float* red = (float*)smem;  // [NW][16][64] accumulators, then [NW][32] column sums
+#pragma unroll
+  for (int e = 0; e < 16; ++e) red[(wave * 16 + e) * 64 + lane] = acc[e];
+  if (want_cs) {
+    const float v = cs + __shfl_xor(cs, 32, 64);
+    if (lane < 32) red[NW * 1024 + wave * 32 + lane] = v;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < 1024; idx += NW * 64) {
+    const int e = idx >> 6, l = idx & 63;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[(w * 16 + e) * 64 + l];
+    const int o = o0 + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5), i = i0 + (l & 31);
+    float* dst = out + (long long)o * ldo + i;
+    *dst = beta != 0.0f ? v + beta * *dst : v;
+  }
+  if (want_cs && tid < 32) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[NW * 1024 + w * 32 + tid];
+    db[o0 + tid] = v;
+  }
+}
+
 int n_workgroups(long long M, long long& rows_per) {
   static int n_cu = 0;
   if (!n_cu) {
@@ -234,6 +337,38 @@ int launch(const bf16* dy, long long ldy, const bf16* x, long long ldx, long lon
   return 0;
 }
 }  // namespace
+
+extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O,
+                                int32_t I, float* out, float beta, float* db, void* stream) {
+  OCTSAM_CHECK_ARG(dy && x && out && M > 0 && M < (1LL << 24) && O > 0 && I > 0 && O % 32 == 0 && I % 32 == 0,
+                   "octsam_wgrad_tok: M=%lld O=%d I=%d (O, I multiples of 32)", (long long)M, O, I);
+  OCTSAM_CHECK_ARG(ldy >= O && ldx >= I && ldy % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)dy & 15) == 0 &&
+                       ((uintptr_t)x & 15) == 0 && (long long)M * ldy * 2 < (1LL << 31) && (long long)M * ldx * 2 < (1LL << 31),
+                   "octsam_wgrad_tok: ldy / ldx multiples of 8, operands 16-B aligned");
+  const int tiles = (O / 32) * (I / 32);
+  hipStream_t s = (hipStream_t)stream;
+  if (M > 1024) {
+    constexpr int NW = 8, LDS = NW * tok::NST * tok::STB;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)wgrad_tok_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(wgrad_tok_kernel<NW>, dim3(tiles), dim3(NW * 64), LDS, s, (const bf16*)dy, (long long)ldy,
+                       (const bf16*)x, (long long)ldx, (long long)M, I / 32, out, I, beta, db);
+  } else {
+    constexpr int NW = 4, LDS = NW * tok::NST * tok::STB;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)wgrad_tok_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(wgrad_tok_kernel<NW>, dim3(tiles), dim3(NW * 64), LDS, s, (const bf16*)dy, (long long)ldy,
+                       (const bf16*)x, (long long)ldx, (long long)M, I / 32, out, I, beta, db);
+  }
+  OCTSAM_LAUNCH_CHECK("octsam_wgrad_tok");
+  return 0;
+}
 
 extern "C" int32_t octsam_wgrad_supported(int64_t M, int32_t O, int32_t I) {
   return M > 0 && (O == 128 || O == 256 || O == 384) && (I == 128 || I == 256) ? 1 : 0;

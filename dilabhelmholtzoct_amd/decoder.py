@@ -271,6 +271,9 @@ class MaskDecoder(nn.Module):
     # image-side weight gradients through octsam_wgrad (False: the split-K tile GEMM + reduction; A/B,
     # scripts/dw_ab.py / scripts/step_ab3.py)
     wide_wgrad = True
+    # token-side weight + bias gradients through octsam_wgrad_tok (False: split-K tile GEMM + reduction + column-sum
+    # kernel + reduction; A/B, scripts/step_ab3.py)
+    tok_wgrad = True
 
     @staticmethod
     def _pick_split(Mtok, O, I):
@@ -320,11 +323,20 @@ class MaskDecoder(nn.Module):
             # image side: one workgroup per CU holds the whole O x I output and streams its rows (octsam_wgrad)
             K.wgrad(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db, dbx=dbx, dbx_fold=dbx_fold)
             return out
+        if (split is None and self.tok_wgrad and M < 65536 and dbx is None and O % 32 == 0 and I % 32 == 0 and ldy % 8 == 0
+                and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and out.is_contiguous()):
+            # token side (and image-side products over fewer rows): weight and bias gradient in one launch
+            # (octsam_wgrad_tok)
+            K.wgrad_tok(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db)
+            return out
         if split is None:
             split, Ks = self._pick_split(M, O, I)
         else:
             Ks = M // split
         dev = out.device
+        if db is not None and M < 65536:  # (the small-problem tile kernel has no fused column sums)
+            K.colsum(dy if ldy == O else dy.view(M, ldy)[:, :O].contiguous(), M, O, db)
+            db = None
         pa = torch.empty((split, O), device=dev, dtype=torch.float32) if db is not None else None
         pb = torch.empty((split, I), device=dev, dtype=torch.float32) if dbx is not None else None
         if split == 1 and Ks == M:
@@ -368,7 +380,7 @@ class MaskDecoder(nn.Module):
         return out
 
     def _lin_bwd(self, dy_b, x_b, wname, bname, M, *, dx_out=None, dx_beta=0.0, ldy=None, ldx=None, x_add=None,
-                 x_add_rows=0, wgroup=None, bgroup=None, db_src=None, ldc=None):
+                 x_add_rows=0, wgroup=None, bgroup=None, ldc=None):
         """Backward of y = x W^T + b: dx (optional, accumulate with dx_beta), dW, db."""
         if wgroup is None:
             w = self.W(wname)
@@ -381,15 +393,9 @@ class MaskDecoder(nn.Module):
         if dx_out is not None:
             self._dx(dy_b, w, M, dx_out, ldy=ldy, beta=dx_beta, ldc=ldc)
         gb = self.G(bname) if bgroup is None else self._group(self.flat_grad, bgroup, 0)
-        if M >= 65536 and db_src is None:  # image side: the bias gradient rides on the weight gradient's pass
-            self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows, db=gb)
-            return
-        self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows)
-        src = dy_b if db_src is None else db_src
-        if ldy == O or db_src is not None:
-            K.colsum(src, M, O, gb)
-        else:
-            K.colsum(dy_b.view(M, ldy)[:, :O].contiguous(), M, O, gb)
+        # the bias gradient rides on the weight gradient's pass over dy (image side: octsam_wgrad's column sums; token
+        # side: octsam_wgrad_tok)
+        self._dw(dy_b, x_b, M, gw, ldy=ldy, ldx=ldx, x_add=x_add, x_add_rows=x_add_rows, db=gb)
 
     def _ln(self, x, prefix, eps, rows, *, f32_out=True):
         w, b = self.Bf(prefix + ".weight"), self.Bf(prefix + ".bias")

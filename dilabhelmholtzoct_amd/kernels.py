@@ -117,6 +117,22 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, M: int, out: torch.Tensor, *, ldy: 
     return out
 
 
+def wgrad_tok(dy: torch.Tensor, x: torch.Tensor, M: int, out: torch.Tensor, *, ldy: int | None = None,
+              ldx: int | None = None, beta: float = 0.0, db: torch.Tensor | None = None) -> torch.Tensor:
+    """Token-side weight gradient in one launch: out[O, I] = beta * out + dy[M, O]^T x[M, I], db = column sums of dy
+    (octsam_wgrad_tok; bf16 operands with row strides ldy / ldx, fp32 out / db)."""
+    _require_cuda(dy, x, out, db)
+    O, I = out.shape
+    ldy = O if ldy is None else ldy
+    ldx = I if ldx is None else ldx
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("wgrad_tok: bf16 operands and a contiguous fp32 output")
+    if db is not None and (db.dtype != torch.float32 or not db.is_contiguous()):
+        raise ValueError("wgrad_tok: db must be contiguous fp32")
+    _lib.call("octsam_wgrad_tok", ptr(dy), ldy, ptr(x), ldx, M, O, I, ptr(out), beta, ptr(db))
+    return out
+
+
 def ph_max_pairs(H: int, W: int) -> int:
     """Pair-buffer length that no [H, W] map can overflow: finite H0 pairs are born at regional minima
     (pairwise non-8-adjacent, <= ceil(H/2)*ceil(W/2)) and H1 pairs die at regional maxima (pairwise

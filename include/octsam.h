@@ -110,6 +110,12 @@ int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t s
  * byte read once); per-workgroup partials are combined in fixed order (deterministic).
  * workspace: octsam_wgrad_workspace(M, O, I) bytes. */
 int32_t octsam_wgrad_supported(int64_t M, int32_t O, int32_t I);
+/* The token-side form (the P*T prompt-token rows of the decoder's token projections / MLPs / hypernetworks, M < 2^24):
+ *   out[o][i] = beta*out[o][i] + sum_m dy[m*ldy + o] * x[m*ldx + i];  db[o] = sum_m dy[m*ldy + o] (optional)
+ * in one launch (one 32x32 output tile per workgroup, its waves splitting the rows, fixed-order combine through LDS:
+ * deterministic). O, I multiples of 32; ldy, ldx multiples of 8; dy, x 16-B aligned. */
+int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I,
+                     float* out, float beta, float* db, void* stream);
 int64_t octsam_wgrad_workspace(int64_t M, int32_t O, int32_t I);
 int octsam_wgrad(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I, float* out,
                  float beta, float* db, float* dbx, int32_t dbx_fold, void* workspace, int64_t workspace_bytes,

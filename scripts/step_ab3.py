@@ -1,8 +1,8 @@
 """Same-process A/B of the pipelined training step (bench.py's loop: hipGraphs + encoder lookahead, B = 8 boxes,
---top=True) for: the topological forward (resampling, persistence, W2) forked beside the DiceCE backward (default),
-only the W2 forked (persistence in F), the W2 on the host between the graphs (w2_host), and the token-side weight
-gradients as one GEMM each instead of split-K + reduction (device_tok_dw_1pass). Interleaved rounds,
-median of 5 rounds x 20 steps. Diagnostic only."""
+--top=True) for variants of the step / mask decoder set while the graphs are captured (STEP_VARIANTS: default,
+wgrad_off = image-side weight gradients by the split-K tile GEMM, tok_off = token-side ones by the split-K tile
+GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence forked beside
+the DiceCE backward too). Interleaved rounds, median of 5 rounds x 20 steps. Diagnostic only."""
 import json
 import os
 import statistics
@@ -25,15 +25,23 @@ def main():
     model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(dev)
     variants = {}
     dec = model.mask_decoder
-    for name, w2, fork, tok_split in (("device", "device", True, True), ("device_ph_in_F", "device", False, True),
-                                      ("w2_host", "host", True, True), ("device_tok_dw_1pass", "device", True, False)):
-        st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True, pipeline=True, w2=w2)
-        st.fork_topo = fork
-        dec.token_dw_split = tok_split  # read while the graphs are captured
+    # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
+    VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
+                "fork_topo": ({"fork_topo": True}, {})}
+    for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
+        st_attr, dec_attr = VARIANTS[name]
+        st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True,
+                            pipeline=os.environ.get("STEP_PIPELINE", "1") == "1")
+        for k, v in st_attr.items():
+            setattr(st, k, v)
+        saved = {k: getattr(dec, k) for k in dec_attr}
+        for k, v in dec_attr.items():
+            setattr(dec, k, v)
         for i in range(3):  # capture + warm
             st.step(batch, next_batch=batch if i < 2 else None)
         st.flush()
-        dec.token_dw_split = True
+        for k, v in saved.items():
+            setattr(dec, k, v)
         variants[name] = st
     torch.cuda.synchronize()
     res = {k: [] for k in variants}

@@ -570,3 +570,34 @@ def test_wgrad_rejects_unsupported(cuda):
     x = torch.zeros(1000, 256, device=cuda, dtype=torch.bfloat16)
     with pytest.raises(OctsamError):
         kernels.wgrad(dy, x, 1000, torch.empty(192, 256, device=cuda))
+
+
+@pytest.mark.parametrize("M,O,I,ldy_pad,ldx_pad,db,beta", [
+    (1176, 256, 256, 0, 0, True, 0.0),    # P*7 token rows (P = 168)
+    (1176, 128, 256, 128, 0, True, 1.0),  # strided dY (a column slice), accumulate
+    (168, 256, 256, 0, 1536, True, 0.0),  # hypernetwork MLP rows (P), X a slice of [P, T*C]
+    (1176, 2048, 256, 0, 0, True, 0.0),   # MLP lin1
+    (1176, 256, 2048, 0, 0, False, 0.0),  # MLP lin2
+    (1, 64, 32, 0, 0, True, 0.0),
+    (100, 32, 96, 8, 8, True, 1.0),       # fewer rows than waves x 32
+    (5000, 96, 64, 0, 0, True, 0.0),
+])
+def test_wgrad_tok(cuda, M, O, I, ldy_pad, ldx_pad, db, beta):
+    """octsam_wgrad_tok (token-side dW = dY^T X + bias column sums, one launch) vs torch fp32 on the same bf16
+    operands; the fixed-order combine is bitwise repeatable."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(M + O + I + ldx_pad)
+    ldy, ldx = O + ldy_pad, I + ldx_pad
+    dy = torch.randn(M, ldy, generator=g).to(cuda, torch.bfloat16)
+    x = torch.randn(M, ldx, generator=g).to(cuda, torch.bfloat16)
+    out0 = torch.randn(O, I, generator=g).to(cuda)
+    out = out0.clone()
+    gdb = torch.full((O,), 7.0, device=cuda) if db else None
+    kernels.wgrad_tok(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=gdb)
+    ref = dy[:, :O].float().t() @ x[:, :I].float() + beta * out0
+    assert _rel(out, ref) < 1e-5
+    if db:
+        assert _rel(gdb, dy[:, :O].float().sum(0)) < 1e-5
+    again = out0.clone()
+    kernels.wgrad_tok(dy, x, M, again, ldy=ldy, ldx=ldx, beta=beta)
+    assert torch.equal(again, out)
