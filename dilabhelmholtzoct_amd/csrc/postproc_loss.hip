@@ -71,11 +71,14 @@ __global__ __launch_bounds__(256) void postproc_fwd_kernel(const float* __restri
   const int nr = min(PP_ROWS, pp.oh - i0);
   const float* x = low + (long long)m * pp.S * pp.S;
   // low-res row range of the group: rows are monotone in i, so the first row's lowest and the last row's
-  // highest source bound it
+  // highest source bound it; only those rows are staged (staging all PP_LRMAX rows read ~5x the low-res bytes:
+  // 382 MB fetched per launch against 87 MB compulsory, profiles/r03/traffic_kernels_r03r.txt)
   const int lo = lin_acf(lin_acf(i0, pp.ch, pp.s2h).i0, pp.S, pp.s1).i0;
-  for (int e = tid; e < PP_LRMAX * 64; e += 256) {
+  const int hi = lin_acf(lin_acf(i0 + nr - 1, pp.ch, pp.s2h).i1, pp.S, pp.s1).i1;
+  const int nlr = min(hi - lo + 1, PP_LRMAX);
+  for (int e = tid; e < nlr * 64; e += 256) {
     const int r = e >> 6, c4 = (e & 63) * 4;
-    if (c4 < pp.S && lo + r < pp.S) *(float4*)&rows[r][c4] = *(const float4*)(x + (long long)(lo + r) * pp.S + c4);
+    if (c4 < pp.S) *(float4*)&rows[r][c4] = *(const float4*)(x + (long long)(lo + r) * pp.S + c4);
   }
   __syncthreads();
   float si = 0.0f, st = 0.0f, sp = 0.0f;
