@@ -1388,11 +1388,19 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
 // EPI < 0: LDS-staged epilogue; EPI >= 0: register epilogue with activation EPI (operand-swapped MFMA).
 // FE: 0 = general register epilogue, else the lean buffer epilogue of that kind (epilogue_fast; needs
 // N % 256 == 0; one epilogue per instantiation keeps the register allocation spill-free)
+// DBG 3 (diagnostics, octsam_gemm_debug_stamps): per workgroup s_memtime at entry, after the main loop and after
+// the epilogue's stores have completed, plus the hardware ids (XCC, CU) -- how long each phase takes in the real
+// kernel and how aligned the workgroups' epilogues are across the chip.
+constexpr int STAMP_WG = 8192;
+__device__ long long g_stamps[STAMP_WG * 4];
+
 template <int DBG, int EPI, int FE = 0>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   constexpr bool TR = EPI >= 0;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  long long st0 = 0, st1 = 0;
+  if constexpr (DBG == 3) st0 = __builtin_amdgcn_s_memtime();
   const int wr = wave >> 2, wc = wave & 3;
   int bid = blockIdx.x;
   {
@@ -1488,6 +1496,7 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   }
   if (wr == 0) raw_barrier();  // balance the stagger
   if (DBG == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DBG == 3) st1 = __builtin_amdgcn_s_memtime();
   if (DBG == 1) {
     float x = 0.f;
 #pragma unroll
@@ -1508,6 +1517,20 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
     }
   } else {
     ph8::epilogue_lds(p, acc, bz, row0, col0, wr, wc, wave, lane, gsm);
+  }
+  if constexpr (DBG == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const long long st2 = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && blockIdx.x < STAMP_WG) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+      long long* d = g_stamps + 4 * blockIdx.x;
+      d[0] = st0;
+      d[1] = st1;
+      d[2] = st2;
+      d[3] = ((long long)xcc << 32) | hw;
+    }
   }
 }
 
@@ -1803,8 +1826,14 @@ constexpr int KS = 32, NS = 3, A_BYTES = 256 * KS * 2, B_BYTES = 128 * KS * 2, S
 constexpr int LDS = NS * STAGE;
 constexpr int OPS = 6;  // LDS-DMA issues per wave per stage: A 16 KiB + B 8 KiB = 24 x 1 KiB over 4 waves
 
+// [row][32] e16 images (64-B rows), 16-B chunk k stored at position k ^ swz(row). The 16x16x32 fragment read
+// (lane: row lane & 15, chunk lane >> 4) meets ds_read_b128's lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
+// (MI355X_MICROARCH.md §LDS): for a fixed row & 3 each group holds four (row group, chunk) pairs, which land on
+// distinct 16-B bank slots iff swz = [0, 3, 2, 1] over (row >> 2) & 3 (sw_off<32>'s (row >> 2) & 3 puts two of them
+// on one slot: 2-way conflicts, SQ_LDS_BANK_CONFLICT = 1/3 of the LDS cycles, profiles/r03/gemm4x_pmc_*.txt).
+__device__ __forceinline__ int swz(int r) { return (-(r >> 2)) & 3; }
 // per-lane source of each of the wave's 6 issues (16 rows x 64 B per issue, [row][32] image with the 16-B chunk
-// index XOR-swizzled by (row >> 2) & 3 — sw_off<32> — applied to the source: the LDS image stays lane-linear)
+// index XOR-swizzled by swz(row) applied to the source: the LDS image stays lane-linear)
 struct Src {
   const e16* p[OPS];
 };
@@ -1817,7 +1846,7 @@ __device__ __forceinline__ Src make_src(const GemmK& p, const e16* A, const e16*
     const bool isA = u < 4;
     const int j = isA ? wave * 4 + u : wave * 2 + (u - 4);
     const int r = j * 16 + rr;
-    const int c = slot ^ ((r >> 2) & 3);
+    const int c = slot ^ swz(r);
     const int lim = isA ? p.M : p.N;
     int g = (isA ? row0 : col0) + r;
     g = g < lim ? g : lim - 1;  // rows past M / N: any valid row (never stored)
@@ -1835,7 +1864,7 @@ __device__ __forceinline__ void stage(const Src& s, int k0, char* buf, int wave)
   }
 }
 __device__ __forceinline__ e16x8 frag(const char* img, int row, int kc) {
-  return *(const e16x8*)(img + sw_off<32>(row, kc));
+  return *(const e16x8*)(img + row * 64 + ((kc ^ swz(row)) << 4));
 }
 }  // namespace g4
 
@@ -1939,6 +1968,13 @@ inline bool prefer_n192(const octsam_gemm_args* a, int n_cu) {
 
 template <int DBG, int EPI>
 int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
+  if constexpr (EPI >= 0 && DBG == 3) {  // stamps: the lean epilogue kinds of the encoder
+    switch (k.fast_epi) {
+      case 1: return launch_gemm8_fe<DBG, EPI, 1>(k, a, s);
+      case 4: return launch_gemm8_fe<DBG, EPI, 4>(k, a, s);
+      default: break;
+    }
+  }
   if constexpr (EPI >= 0 && DBG == 0) {
     static int n_cu = 0;
     if (!n_cu) {
@@ -2279,6 +2315,12 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
+extern "C" int octsam_gemm_debug_stamps(int64_t* host, int32_t n_wg) {
+  OCTSAM_CHECK_ARG(host && n_wg > 0 && n_wg <= STAMP_WG, "octsam_gemm_debug_stamps: bad args");
+  const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n_wg * 4 * sizeof(long long));
+  OCTSAM_CHECK_ARG(e == hipSuccess, "octsam_gemm_debug_stamps: %s", hipGetErrorString(e));
+  return 0;
+}
 #endif
 
 extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
@@ -2382,6 +2424,10 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       if (g_use_glds == 6) return launch_gemm8<1, 0>(k, a, s);
       if (g_use_glds == 7) return launch_gemm8<2, 0>(k, a, s);
       if (g_use_glds == 8) return launch_gemm8<0, -1>(k, a, s);
+      if (g_use_glds == 9) {  // stamped one-tile-per-workgroup kernel (diagnostics)
+        if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<3, OCTSAM_ACT_GELU>(k, a, s);
+        return launch_gemm8<3, 0>(k, a, s);
+      }
       // persistent variant: bias / activation epilogues (no residual or row map loads in the epilogue);
       // fast path 11 forces the one-tile-per-workgroup kernel (A/B diagnostics)
       // (an e16 residual is allowed at small K: its loads drain the next tile's prefetch, which is the whole

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 14
+#define OCTSAM_ABI_VERSION 15
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -96,6 +96,10 @@ void octsam_gemm_set_fast_path(int32_t enable);
 /* 1 if the calling thread's last octsam_gemm launched the persistent global_load_lds kernel
    (gemm_glds_kernel), 0 for the generic tile kernel. Used to attribute per-kernel timings. */
 int32_t octsam_gemm_last_path(void);
+/* diagnostics: fast path 9 runs the one-tile-per-workgroup 8-phase kernel with per-workgroup s_memtime stamps
+   (entry, main loop done, epilogue stores done) and hardware ids; this copies the first n_wg workgroups' records
+   (4 x int64 each: t0, t1, t2, XCC_ID << 32 | HW_ID) to host memory (synchronous) */
+int octsam_gemm_debug_stamps(int64_t* host, int32_t n_wg);
 
 /* out[i] = sum_{s<splits} partials[s*n+i] + beta*out[i]  (fp32; deterministic split-K combine) */
 int octsam_splitk_reduce(const float* partials, float* out, int64_t n, int32_t splits, float beta, void* stream);
