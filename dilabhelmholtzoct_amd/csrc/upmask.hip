@@ -41,6 +41,28 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_mov<0x128>(v);  // row_ror:8
   return v;
 }
+// Reduce-scatter over the 16 lanes of a row: lane c returns sum over the row's lanes of v[c] (4 DPP exchange stages
+// pairing c with c ^ 8, c ^ 7, c ^ 3, c ^ 1, each lane keeping the half its bit selects). Fixed order: deterministic.
+__device__ __forceinline__ float row16_reduce_scatter(const float (&v)[16], int c) {
+  float a[8], b[4], d[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool hi = c & 8;
+    a[k] = (hi ? v[8 + k] : v[k]) + dpp_mov<0x128>(hi ? v[k] : v[8 + k]);  // row_ror:8 (c ^ 8)
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool hi = c & 4;
+    b[k] = (hi ? a[4 + k] : a[k]) + dpp_mov<0x141>(hi ? a[k] : a[4 + k]);  // row_half_mirror (c ^ 7)
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool hi = c & 2;
+    d[k] = (hi ? b[2 + k] : b[k]) + dpp_mov<0x1B>(hi ? b[k] : b[2 + k]);  // quad_perm [3,2,1,0] (c ^ 3)
+  }
+  const bool hi = c & 1;
+  return (hi ? d[1] : d[0]) + dpp_mov<0xB1>(hi ? d[0] : d[1]);  // quad_perm [1,0,3,2] (c ^ 1)
+}
 __device__ __forceinline__ float xor16_value(float x, bool hi) {
   const uint32_t u = __builtin_bit_cast(uint32_t, x);
   const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
@@ -244,17 +266,35 @@ __device__ __forceinline__ void load_ublk(const bf16* __restrict__ up1, long lon
 }
 }  // namespace um
 
+// LN = true: the LayerNorm2d + GELU in front of up1 (up1 = GELU(LN(x)), hf:modeling_sam.py:519-520) is
+// differentiated in the same pass, so d up1 never reaches HBM: with x the ConvT1 output row (bf16 [rows][64]),
+// mean / rstd its saved statistics, xh = (x - mean) rstd and y = xh w + b,
+//   gy = d up1 * GELU'(y),  g = gy w,  dx = rstd (g - mean_c(g) - xh mean_c(g xh)),
+//   d w_c += gy xh, d b_c += gy  (fixed-order per-workgroup partials, part_ln [grid][2][64])
+// — ln_bwd_kernel's arithmetic on the fp32 d up1 instead of its bf16 copy. A row's 64 channels are the 16 of each
+// of the lanes c, c + 16, c + 32, c + 48, so the two row sums take one permlane16 and one permlane32 swap; the
+// per-channel d w / d b sums over a tile's rows are one DPP reduce-scatter each (two accumulators per lane).
+struct LnArgs {
+  const bf16* x;
+  const float* mean;
+  const float* rstd;
+  const float* w;
+  const float* b;
+  float* part;
+};
 // part_h fp32 [256][P * NS * 32] (per tile-in-prompt), part_w [grid][64][128], part_b [grid][32]
-template <int NS>
+template <int NS, bool LN>
 __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restrict__ up1, const bf16* __restrict__ w2,
                                                             const float* __restrict__ b2,
                                                             const float* __restrict__ hyper,
                                                             const float* __restrict__ dmask, int ntiles, int P,
                                                             bf16* __restrict__ dup1, float* __restrict__ part_h,
-                                                            float* __restrict__ part_w, float* __restrict__ part_b) {
+                                                            float* __restrict__ part_w, float* __restrict__ part_b,
+                                                            LnArgs ln) {
   using namespace um;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_red = (float*)(smem + S_DM + NS * 1024);  // [4 waves][NS * 32]
+  float* s_ln = s_red + 4 * NS * 32;                 // LN: w [64], b [64], then [4 waves][2][64] partials
   float* scratch = part_b + gridDim.x * 32 + blockIdx.x * 256;  // sink of the idle threads' partial stores
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   // W2^T fragments for d up1 = dpre W2^T: fragment (m, kb), lane (g, c), element j = w2[k = 16 kb + c][n],
@@ -276,6 +316,12 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
     *(bf16x8*)(smem + S_W2 + 16 * e) = v;
   }
   if (tid < 128) ((float*)(smem + S_BIAS))[tid] = b2[tid & 31];
+  if constexpr (LN) {
+    if (tid < 128) s_ln[tid] = tid < 64 ? ln.w[tid] : ln.b[tid - 64];
+  }
+  // d w / d b of LayerNorm channel 16 (c >> 2) + 4 g + (c & 3), summed over the rows of this lane's row group (lanes
+  // 16 g .. 16 g + 15 of the wave) and every tile (one reduce-scatter per tile)
+  float lnw_acc = 0.0f, lnb_acc = 0.0f;
   f32x4 dwacc[4][2];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) dwacc[kb][0] = dwacc[kb][1] = (f32x4)0.0f;
@@ -298,6 +344,16 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
   if (T >= ntiles) return;
   prefetch(T, ua, da_);
   auto step = [&](const bf16x8 (&ub)[2], const float (&dcur)[NS], bf16x8 (&nu)[2], float (&nd)[NS], int T) {
+    // LN: the lane's x (ConvT1 output) row segments and row statistics, loaded at the tile's start (consumed after
+    // its ConvT2 recompute and d up1 products; a prefetch one tile ahead would not fit the registers)
+    uint2 xc[LN ? 4 : 1];
+    float2 sc;
+    if constexpr (LN) {
+      const long long orow = (long long)T * BROWS + 16 * w + c;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) xc[kb] = *(const uint2*)(ln.x + orow * 64 + 16 * kb + 4 * g);
+      sc = make_float2(ln.mean[orow], ln.rstd[orow]);
+    }
     const int p = T / BTILES_PER_P;
     const int rr = 16 * w + c;
     f32x4 hy[NS][2];
@@ -377,16 +433,6 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
       for (int kb = 0; kb < 4; ++kb)
         da[kb] = mfma32(*(const bf16x8*)(smem + S_W2T + 16 * ((4 * m + kb) * 64 + lane)), bop, da[kb]);
     }
-    {
-      const long long orow = (long long)T * BROWS + rr;
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        bf16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (bf16)da[kb][i];
-        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
-      }
-    }
     // d hyper of this tile: sum over the 16 rows of each lane group (the 4 waves are summed after (C))
 #pragma unroll
     for (int t = 0; t < NS; ++t)
@@ -398,6 +444,61 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
           v = row16_sum(v);
           if (c == 0) s_red[w * NS * 32 + t * 32 + 16 * hh + 4 * g + i] = v;
         }
+    // d x (LN) / d up1 rows, after the d hyper sums so their registers are free
+    if constexpr (LN) {  // d up1 -> d x through GELU and LayerNorm2d (see LnArgs)
+      const long long orow = (long long)T * BROWS + rr;
+      const float mu = sc.x, rs = sc.y;
+      auto xnorm = [&](int kb, int i) {
+        const uint32_t pr = (i & 2) ? xc[kb].y : xc[kb].x;
+        return (__builtin_bit_cast(float, (i & 1) ? (pr & 0xffff0000u) : (pr << 16)) - mu) * rs;
+      };
+      float gy[16], tmp[16];
+      float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const f32x4 lw = *(const f32x4*)(s_ln + 16 * kb + 4 * g), lb = *(const f32x4*)(s_ln + 64 + 16 * kb + 4 * g);
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const f32x2 xn = {xnorm(kb, i), xnorm(kb, i + 1)};
+          f32x2 u, du;
+          gelu2<true>(fma2(xn, f32x2{lw[i], lw[i + 1]}, f32x2{lb[i], lb[i + 1]}), u, du);
+          const f32x2 gv = f32x2{da[kb][i], da[kb][i + 1]} * du;
+          gy[4 * kb + i] = gv.x;
+          gy[4 * kb + i + 1] = gv.y;
+          const f32x2 gw = gv * f32x2{lw[i], lw[i + 1]};
+          s1 += gw.x + gw.y;
+          s2 += gw.x * xn.x + gw.y * xn.y;
+          tmp[4 * kb + i] = gv.x * xn.x;
+          tmp[4 * kb + i + 1] = gv.y * xn.y;
+        }
+      }
+      lnw_acc += row16_reduce_scatter(tmp, c);
+      lnb_acc += row16_reduce_scatter(gy, c);
+      // row sums over the 4 lanes holding the row's 64 channels (same value in all four: + is commutative)
+      s1 += xor16_value(s1, g & 1);
+      s2 += xor16_value(s2, g & 1);
+      s1 += xor32_value(s1, g >> 1);
+      s2 += xor32_value(s2, g >> 1);
+      s1 *= 1.0f / 64.0f;
+      s2 *= 1.0f / 64.0f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const f32x4 lw = *(const f32x4*)(s_ln + 16 * kb + 4 * g);
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)(rs * (gy[4 * kb + i] * lw[i] - s1 - xnorm(kb, i) * s2));
+        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
+      }
+    } else {
+      const long long orow = (long long)T * BROWS + rr;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)da[kb][i];
+        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
+      }
+    }
     __syncthreads();  // (C) dpre tile and d hyper rows complete
     {
       const int j = tid < NS * 32 ? tid : 0;
@@ -446,6 +547,16 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
     }
   __syncthreads();
   if (tid < 32) part_b[blockIdx.x * 32 + tid] = s_red[tid] + s_red[32 + tid] + s_red[64 + tid] + s_red[96 + tid];
+  if constexpr (LN) {  // d w / d b of the LayerNorm: rows of the wave (lanes c) by DPP, the 4 waves through LDS
+    float* s_lp = s_ln + 128;  // [4][128]
+    const int ch = 16 * (c >> 2) + 4 * g + (c & 3);
+    s_lp[w * 128 + ch] = lnw_acc;
+    s_lp[w * 128 + 64 + ch] = lnb_acc;
+    __syncthreads();
+    if (tid < 128)
+      ln.part[(tid >> 6) * gridDim.x * 64 + blockIdx.x * 64 + (tid & 63)] =
+          s_lp[tid] + s_lp[128 + tid] + s_lp[256 + tid] + s_lp[384 + tid];
+  }
 }
 
 int g_fwd_grid = 768, g_bwd_grid = um::NWG;  // persistent grids (octsam_upmask_set_grid: tuning)
@@ -481,8 +592,40 @@ extern "C" int octsam_upmask_fwd(const void* up1, const void* w2, const float* b
 extern "C" int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok) {
   if (P <= 0 || ntok <= 0) return 0;
   const long long grid = upmask_grid(P * um::BTILES_PER_P, um::NWG);
-  return (long long)um::BTILES_PER_P * P * ntok * 32 + grid * 8192 + grid * 32 + grid * 256;
+  // part_h, part_w, part_b, the idle threads' sink (grid * 256), the LayerNorm partials (grid * 128)
+  return (long long)um::BTILES_PER_P * P * ntok * 32 + grid * 8192 + grid * 32 + grid * 256 + grid * 128;
 }
+
+namespace {
+int upmask_bwd_impl(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask, int32_t P,
+                    int32_t ntok, void* dout, float* dw2, float* db2, float* dhyper, float* workspace, const LnArgs* ln,
+                    float* dlnw, float* dlnb, void* stream) {
+  const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles, g_bwd_grid);
+  float* part_h = workspace;
+  float* part_w = part_h + (long long)um::BTILES_PER_P * P * ntok * 32;
+  float* part_b = part_w + (long long)grid * 8192;
+  LnArgs la = ln ? *ln : LnArgs{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  la.part = part_b + (long long)grid * 32 + (long long)grid * 256;  // [2][grid][64]
+  hipStream_t s = (hipStream_t)stream;
+  const int lds = um::S_DM + ntok * 1024 + 4 * ntok * 32 * 4 + (ln ? (128 + 512) * 4 : 0);
+#define UM_BWD(NS, L)                                                                                            \
+  hipLaunchKernelGGL((upmask_bwd_kernel<NS, L>), dim3(grid), dim3(256), lds, s, (const bf16*)up1, (const bf16*)w2, b2, \
+                     hyper, dmask, ntiles, P, (bf16*)dout, part_h, part_w, part_b, la)
+  if (ntok == 1) {
+    if (ln) UM_BWD(1, true); else UM_BWD(1, false);
+  } else {
+    if (ln) UM_BWD(3, true); else UM_BWD(3, false);
+  }
+#undef UM_BWD
+  OCTSAM_LAUNCH_CHECK("octsam_upmask_bwd");
+  int rc = octsam_splitk_reduce(part_h, dhyper, (int64_t)P * ntok * 32, um::BTILES_PER_P, 0.0f, stream);
+  if (!rc) rc = octsam_splitk_reduce(part_w, dw2, 8192, grid, 0.0f, stream);
+  if (!rc) rc = octsam_splitk_reduce(part_b, db2, 32, grid, 0.0f, stream);
+  if (!rc && ln) rc = octsam_splitk_reduce(la.part, dlnw, 64, grid, 0.0f, stream);
+  if (!rc && ln) rc = octsam_splitk_reduce(la.part + (long long)grid * 64, dlnb, 64, grid, 0.0f, stream);
+  return rc;
+}
+}  // namespace
 
 extern "C" int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper,
                                  const float* dmask, int32_t P, int32_t ntok, void* dup1, float* dw2, float* db2,
@@ -493,21 +636,22 @@ extern "C" int octsam_upmask_bwd(const void* up1, const void* w2, const float* b
   OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
                        ((uintptr_t)dup1 & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
                    "octsam_upmask_bwd: misaligned operand");
-  const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles, g_bwd_grid);
-  float* part_h = workspace;
-  float* part_w = part_h + (long long)um::BTILES_PER_P * P * ntok * 32;
-  float* part_b = part_w + (long long)grid * 8192;
-  hipStream_t s = (hipStream_t)stream;
-  const int lds = um::S_DM + ntok * 1024 + 4 * ntok * 32 * 4;
-  if (ntok == 1)
-    hipLaunchKernelGGL(upmask_bwd_kernel<1>, dim3(grid), dim3(256), lds, s, (const bf16*)up1, (const bf16*)w2, b2,
-                       hyper, dmask, ntiles, P, (bf16*)dup1, part_h, part_w, part_b);
-  else
-    hipLaunchKernelGGL(upmask_bwd_kernel<3>, dim3(grid), dim3(256), lds, s, (const bf16*)up1, (const bf16*)w2, b2,
-                       hyper, dmask, ntiles, P, (bf16*)dup1, part_h, part_w, part_b);
-  OCTSAM_LAUNCH_CHECK("octsam_upmask_bwd");
-  int rc = octsam_splitk_reduce(part_h, dhyper, (int64_t)P * ntok * 32, um::BTILES_PER_P, 0.0f, stream);
-  if (!rc) rc = octsam_splitk_reduce(part_w, dw2, 8192, grid, 0.0f, stream);
-  if (!rc) rc = octsam_splitk_reduce(part_b, db2, 32, grid, 0.0f, stream);
-  return rc;
+  return upmask_bwd_impl(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper, workspace, nullptr, nullptr,
+                         nullptr, stream);
+}
+
+extern "C" int octsam_upmask_ln_bwd(const void* up1, const void* w2, const float* b2, const float* hyper,
+                                    const float* dmask, int32_t P, int32_t ntok, const void* x, const float* mean,
+                                    const float* rstd, const float* ln_w, const float* ln_b, void* dx, float* dw2,
+                                    float* db2, float* dhyper, float* dln_w, float* dln_b, float* workspace,
+                                    void* stream) {
+  OCTSAM_CHECK_ARG(up1 && w2 && b2 && hyper && dmask && x && mean && rstd && ln_w && ln_b && dx && dw2 && db2 &&
+                       dhyper && dln_w && dln_b && workspace && P > 0 && (ntok == 1 || ntok == 3),
+                   "octsam_upmask_ln_bwd: bad args (ntok must be 1 or 3)");
+  OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
+                       ((uintptr_t)dx & 7) == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
+                   "octsam_upmask_ln_bwd: misaligned operand");
+  const LnArgs ln{(const bf16*)x, mean, rstd, ln_w, ln_b, nullptr};
+  return upmask_bwd_impl(up1, w2, b2, hyper, dmask, P, ntok, dx, dw2, db2, dhyper, workspace, &ln, dln_w, dln_b,
+                         stream);
 }

@@ -274,6 +274,9 @@ class MaskDecoder(nn.Module):
     # token-side weight + bias gradients through octsam_wgrad_tok (False: split-K tile GEMM + reduction + column-sum
     # kernel + reduction; A/B, scripts/step_ab3.py)
     tok_wgrad = True
+    # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
+    # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
+    fused_ln_bwd = True
 
     @staticmethod
     def _pick_split(Mtok, O, I):
@@ -592,16 +595,21 @@ class MaskDecoder(nn.Module):
         G.zero_()
         nsel = len(s.sel)
         dm = dmasks.reshape(P, nsel, 65536).contiguous().float()
-        # ---- mask head + ConvT2 (+ GELU), fused: recomputes the ConvT2 product from up1
+        # ---- mask head + ConvT2 (+ GELU), fused: recomputes the ConvT2 product from up1; with fused_ln_bwd the
+        # LayerNorm2d + GELU backward rides in the same pass (d up1 never reaches HBM)
         dhyper = torch.empty(P, nsel, 32, device=dev, dtype=f32)
-        dup1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
-        K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel, dup1,
-                     self.G("upscale_conv2.weight"), self.G("upscale_conv2.bias"), dhyper)
-        # LN2d + GELU
         dup1pre = torch.empty(RL * 4, 64, device=dev, dtype=b16)
-        K.layernorm_bwd(dup1, s.up1pre, s.up_mean, s.up_rstd, self.Bf("upscale_layer_norm.weight"),
-                        self.Bf("upscale_layer_norm.bias"), dup1pre, act=ACT_GELU,
-                        dw=self.G("upscale_layer_norm.weight"), db=self.G("upscale_layer_norm.bias"))
+        lnw, lnb = self.Bf("upscale_layer_norm.weight"), self.Bf("upscale_layer_norm.bias")
+        glnw, glnb = self.G("upscale_layer_norm.weight"), self.G("upscale_layer_norm.bias")
+        if self.fused_ln_bwd:
+            K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel,
+                         dup1pre, self.G("upscale_conv2.weight"), self.G("upscale_conv2.bias"), dhyper,
+                         ln=(s.up1pre, s.up_mean, s.up_rstd, lnw, lnb, glnw, glnb))
+        else:
+            dup1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
+            K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel,
+                         dup1, self.G("upscale_conv2.weight"), self.G("upscale_conv2.bias"), dhyper)
+            K.layernorm_bwd(dup1, s.up1pre, s.up_mean, s.up_rstd, lnw, lnb, dup1pre, act=ACT_GELU, dw=glnw, db=glnb)
         # ConvT1: y[RL, 256] = keys2[RL, 256] @ W1s[256, 256]
         # the image-side keys gradient stream is bf16 (as under the reference's bf16 autocast): it is written,
         # read-modify-written by each block's projection backward and read by LayerNorm4's backward per block

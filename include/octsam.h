@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 15
+#define OCTSAM_ABI_VERSION 16
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -290,6 +290,15 @@ void octsam_upmask_set_grid(int32_t fwd, int32_t bwd);
 int octsam_upmask_bwd(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask,
                       int32_t P, int32_t ntok, void* dup1, float* dw2, float* db2, float* dhyper, float* workspace,
                       void* stream);
+/* octsam_upmask_bwd with the LayerNorm2d(eps) + GELU in front of up1 (up1 = GELU(LN(x)), hf:modeling_sam.py:519-520)
+ * differentiated in the same pass (replaces octsam_upmask_bwd + octsam_layernorm_bwd(act = GELU) over the 64-channel
+ * rows: d up1 is never stored): x bf16 [P*16384, 64] the ConvT1 output, mean / rstd fp32 [P*16384] its LayerNorm
+ * statistics (octsam_layernorm_fwd), ln_w / ln_b fp32 [64]; writes dx bf16 [P*16384, 64] and, overwriting, d w2, d b2,
+ * d hyper, d ln_w, d ln_b fp32 (fixed-order reductions). Same workspace as octsam_upmask_bwd. */
+int octsam_upmask_ln_bwd(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask,
+                         int32_t P, int32_t ntok, const void* x, const float* mean, const float* rstd, const float* ln_w,
+                         const float* ln_b, void* dx, float* dw2, float* db2, float* dhyper, float* dln_w, float* dln_b,
+                         float* workspace, void* stream);
 
 /* ---------------------------------------------------------------- post-processing + losses
  * octsam_postproc_fwd: ref:octsam/models/training_utils.py:57-59 — lowres fp32 [M,S,S] -> bilinear to

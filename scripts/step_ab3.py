@@ -2,7 +2,8 @@
 --top=True) for variants of the step / mask decoder set while the graphs are captured (STEP_VARIANTS: default,
 wgrad_off = image-side weight gradients by the split-K tile GEMM, tok_off = token-side ones by the split-K tile
 GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence forked beside
-the DiceCE backward too). Interleaved rounds, median of 5 rounds x 20 steps. Diagnostic only."""
+the DiceCE backward too, ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
+the mask-head backward). Interleaved rounds, median of 5 rounds x 20 steps. Diagnostic only."""
 import json
 import os
 import statistics
@@ -27,7 +28,7 @@ def main():
     dec = model.mask_decoder
     # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
     VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
-                "fork_topo": ({"fork_topo": True}, {})}
+                "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False})}
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
         st_attr, dec_attr = VARIANTS[name]
         st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True,

@@ -73,3 +73,46 @@ def test_upmask_deterministic(cuda):
         res.append((masks, dup1, dw2, db2, dh))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("P,ns", [(3, 1), (2, 3)])
+def test_upmask_ln_bwd(cuda, P, ns):
+    """octsam_upmask_ln_bwd: the LayerNorm2d(eps 1e-6) + GELU in front of up1 differentiated in the mask-head
+    backward, vs fp32 autograd through LN + GELU + ConvT2 + mask head on the same bf16 x (the kernel's up1 is the
+    bf16 LN forward output, as in the step). d x at 1e-2 of its max (the d pre-activation feeds the MFMAs as bf16),
+    d LN weight / bias at 1e-2; and the fused path against octsam_upmask_bwd + octsam_layernorm_bwd (which rounds
+    d up1 to bf16 in between) at 2e-2."""
+    from dilabhelmholtzoct_amd import kernels
+    _, w2, b2, hyper, dmask = _inputs(cuda, P, ns, 7 * P + ns)
+    g = torch.Generator().manual_seed(5 + P)
+    x = (torch.randn(P * 16384, 64, generator=g) * 0.8 + 0.3).to(cuda, torch.bfloat16)
+    lw = (1.0 + 0.3 * torch.randn(64, generator=g)).to(cuda)
+    lb = (0.2 * torch.randn(64, generator=g)).to(cuda)
+    up1 = torch.empty_like(x)
+    mean = torch.empty(P * 16384, device=cuda)
+    rstd = torch.empty(P * 16384, device=cuda)
+    kernels.layernorm_fwd(x, lw, lb, 1e-6, up1, act=2, mean=mean, rstd=rstd)
+    xr = x.float().requires_grad_()
+    wr, br = lw.clone().requires_grad_(), lb.clone().requires_grad_()
+    u = F.gelu(F.layer_norm(xr, (64,), wr, br, eps=1e-6))
+    ref = _ref(u, w2.float(), b2, hyper, P)
+    (ref * dmask).sum().backward()
+    dx = torch.empty_like(x)
+    dw2, db2, dh = torch.empty(64, 128, device=cuda), torch.empty(32, device=cuda), torch.empty(P, ns, 32, device=cuda)
+    dlw, dlb = torch.full((64,), float("nan"), device=cuda), torch.full((64,), float("nan"), device=cuda)
+    kernels.upmask_bwd(up1, w2, b2, hyper, dmask, P, ns, dx, dw2, db2, dh, ln=(x, mean, rstd, lw, lb, dlw, dlb))
+    assert _rel(dx, xr.grad) < 1e-2, _rel(dx, xr.grad)
+    assert _rel(dlw, wr.grad) < 1e-2, _rel(dlw, wr.grad)
+    assert _rel(dlb, br.grad) < 1e-2, _rel(dlb, br.grad)
+    # the two-kernel path
+    dup1 = torch.empty_like(x)
+    dw2b, db2b, dhb = torch.empty_like(dw2), torch.empty_like(db2), torch.empty_like(dh)
+    kernels.upmask_bwd(up1, w2, b2, hyper, dmask, P, ns, dup1, dw2b, db2b, dhb)
+    dx2 = torch.empty_like(x)
+    _, dlw2, dlb2 = kernels.layernorm_bwd(dup1, x, mean, rstd, lw, lb, dx2, act=2)
+    assert torch.equal(dw2, dw2b) and torch.equal(db2, db2b) and torch.equal(dh, dhb)
+    assert _rel(dx, dx2) < 2e-2 and _rel(dlw, dlw2) < 2e-2 and _rel(dlb, dlb2) < 2e-2
+    # deterministic
+    dx3, dlw3, dlb3 = torch.empty_like(x), torch.empty_like(dlw), torch.empty_like(dlb)
+    kernels.upmask_bwd(up1, w2, b2, hyper, dmask, P, ns, dx3, dw2b, db2b, dhb, ln=(x, mean, rstd, lw, lb, dlw3, dlb3))
+    assert torch.equal(dx, dx3) and torch.equal(dlw, dlw3) and torch.equal(dlb, dlb3)
