@@ -85,8 +85,8 @@ def parse():
 
 def dominant_name(args) -> str:
     e = "bf16" if args.dtype == "bf16" else "fp16 (encoder) / bf16 (decoder)"
-    return (f"gemm8_kernel<0, EPI> (8-phase 256x256 {e} NT GEMM: encoder QKV/proj/MLP, neck, decoder "
-            "projections)")
+    return (f"gemm8_kernel<0, EPI> family (8-phase 256x256 {e} NT GEMM, with its persistent form and the two-"
+            "workgroup 256x128 gemm4w_kernel: encoder QKV/proj/MLP, neck, decoder projections)")
 
 
 class GemmEventTimer:
