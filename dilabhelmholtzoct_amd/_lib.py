@@ -74,6 +74,7 @@ _SIGNATURES = {
     "octsam_colsum": (c_int32, [c_void_p, c_int32, c_int64, c_int32, c_void_p, c_int32, c_void_p]),
     "octsam_prompt_tokens": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_float, c_void_p, c_void_p]),
+    "octsam_mask_embed": (c_int32, [c_void_p, c_int32, c_void_p, c_float, c_void_p, c_void_p]),
     "octsam_image_pe": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "octsam_cast_bf16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "octsam_cast_f16": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),

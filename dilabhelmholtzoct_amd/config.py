@@ -51,6 +51,7 @@ class PromptConfig:
     patch_size: int = 16
     mask_input_channels: int = 16
     num_point_embeddings: int = 4
+    layer_norm_eps: float = 1e-6
 
     @property
     def image_embedding_size(self) -> int:

@@ -189,7 +189,86 @@ __global__ void image_pe_kernel(const float* __restrict__ G, int size, float* __
   pe256(((float)x + 0.5f) / size, ((float)y + 0.5f) / size, G, out + (long long)pix * 256, t);
 }
 
+// SamMaskEmbedding.forward (hf:modeling_sam.py:569-592), the dense prompt of input_masks: conv 2x2/s2 (1 -> 4) ->
+// LayerNorm2d(4) -> GELU -> conv 2x2/s2 (4 -> 16) -> LayerNorm2d(16) -> GELU -> conv 1x1 (16 -> 256). One thread per
+// output pixel of the 64 x 64 grid: its 4 x 4 input patch gives the 2 x 2 first-stage pixels, the second stage and
+// the 1x1 projection stay in registers; the weights are in LDS. masks fp32 [B, 256, 256] -> out fp32 [B, 4096, 256]
+// (pixel-major: the decoder's image-embedding layout). Packed weights wp (fp32): conv1 w [4][4] (o, ky*2+kx), b [4],
+// ln1 w [4], b [4], conv2 w [16][16] (o, c*4 + dy*2 + dx), b [16], ln2 w [16], b [16], conv3 w [256][16], b [256].
+constexpr int ME_W = 16 + 4 + 4 + 4 + 256 + 16 + 16 + 16 + 4096 + 256;
+__device__ __forceinline__ float me_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__global__ __launch_bounds__(256) void mask_embed_kernel(const float* __restrict__ masks, const float* __restrict__ wp,
+                                                         float eps, float* __restrict__ out) {
+  __shared__ float w[ME_W];
+  for (int i = threadIdx.x; i < ME_W; i += 256) w[i] = wp[i];
+  __syncthreads();
+  const float *w1 = w, *b1 = w + 16, *g1 = w + 20, *be1 = w + 24, *w2 = w + 28, *b2 = w + 284, *g2 = w + 300,
+              *be2 = w + 316, *w3 = w + 332, *b3 = w + 332 + 4096;
+  const int b = blockIdx.y, pix = blockIdx.x * 256 + threadIdx.x;  // 16 blocks x 256 = 4096 pixels
+  const int Y = pix >> 6, X = pix & 63;
+  const float* m = masks + (long long)b * 65536;
+  float h1[4][4];  // [2x2 first-stage pixel][channel]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int y = 4 * Y + 2 * (q >> 1), x = 4 * X + 2 * (q & 1);
+    const float in[4] = {m[y * 256 + x], m[y * 256 + x + 1], m[(y + 1) * 256 + x], m[(y + 1) * 256 + x + 1]};
+    float v[4], mu = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      v[o] = b1[o] + w1[o * 4 + 0] * in[0] + w1[o * 4 + 1] * in[1] + w1[o * 4 + 2] * in[2] + w1[o * 4 + 3] * in[3];
+      mu += v[o];
+    }
+    mu *= 0.25f;
+    float var = 0.0f;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) var += (v[o] - mu) * (v[o] - mu);
+    const float rs = 1.0f / sqrtf(var * 0.25f + eps);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) h1[q][o] = me_gelu((v[o] - mu) * rs * g1[o] + be1[o]);
+  }
+  float h2[16], mu = 0.0f;
+#pragma unroll
+  for (int o = 0; o < 16; ++o) {
+    float a = b2[o];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a += w2[o * 16 + c * 4 + q] * h1[q][c];
+    h2[o] = a;
+    mu += a;
+  }
+  mu *= 1.0f / 16.0f;
+  float var = 0.0f;
+#pragma unroll
+  for (int o = 0; o < 16; ++o) var += (h2[o] - mu) * (h2[o] - mu);
+  const float rs = 1.0f / sqrtf(var * (1.0f / 16.0f) + eps);
+#pragma unroll
+  for (int o = 0; o < 16; ++o) h2[o] = me_gelu((h2[o] - mu) * rs * g2[o] + be2[o]);
+  float* o = out + ((long long)b * 4096 + pix) * 256;
+  for (int j = 0; j < 256; j += 4) {
+    float4 r;
+    float* rp = (float*)&r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = b3[j + e];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) a += w3[(j + e) * 16 + c] * h2[c];
+      rp[e] = a;
+    }
+    *(float4*)(o + j) = r;
+  }
+}
+
 }  // namespace
+
+extern "C" int octsam_mask_embed(const float* masks, int32_t B, const float* packed_weights, float eps, float* out,
+                                 void* stream) {
+  OCTSAM_CHECK_ARG(masks && packed_weights && out && B > 0 && B <= 65535, "octsam_mask_embed: bad args");
+  OCTSAM_CHECK_ARG(((uintptr_t)out & 15) == 0, "octsam_mask_embed: out must be 16-B aligned");
+  hipLaunchKernelGGL(mask_embed_kernel, dim3(16, B), dim3(256), 0, (hipStream_t)stream, masks, packed_weights, eps, out);
+  OCTSAM_LAUNCH_CHECK("octsam_mask_embed");
+  return 0;
+}
 
 extern "C" int octsam_axpby(const void* a, int32_t a_f32, const void* b, int32_t b_f32, int64_t b_period, float alpha,
                             float beta, void* out, int32_t out_f32, float* out2_f32, int64_t n, void* stream) {

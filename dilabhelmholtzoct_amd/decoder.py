@@ -448,7 +448,11 @@ class MaskDecoder(nn.Module):
         s.tok0_b = self._bf(tok0)
         imgd = torch.empty(B * L, C, device=dev, dtype=f32)
         imgd_b = torch.empty(B * L, C, device=dev, dtype=b16)
-        K.axpby(emb, no_mask.float().contiguous(), imgd_b, b_period=C, out2_f32=imgd)  # image_embeddings + dense
+        # image_embeddings + dense: no_mask_embed [1, C] broadcast, or a mask prompt's embedding [B, L, C]
+        dense = no_mask.float().contiguous()
+        if dense.numel() not in (C, B * L * C):
+            raise ValueError("dense prompt embedding must be [1, C] or [B, 4096, C]")
+        K.axpby(emb, dense, imgd_b, b_period=C if dense.numel() == C else 0, out2_f32=imgd)
         s.imgd, s.imgd_b = imgd, imgd_b
         pe_b = self._bf(pe)
         s.pe_b = pe_b

@@ -359,6 +359,16 @@ def upmask_bwd(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper, ln=No
     return dup1
 
 
+def mask_embed(masks: torch.Tensor, packed: torch.Tensor, eps: float, out: torch.Tensor) -> torch.Tensor:
+    """SamMaskEmbedding forward (octsam_mask_embed): masks fp32 [B, 256, 256] -> out fp32 [B, 4096, 256]."""
+    _require_cuda(masks, packed, out)
+    B = masks.shape[0]
+    if masks.dtype != torch.float32 or masks.numel() != B * 65536 or out.numel() != B * 4096 * 256:
+        raise ValueError("mask_embed: masks fp32 [B, 256, 256], out fp32 [B, 4096, 256]")
+    _lib.call("octsam_mask_embed", ptr(masks.contiguous()), B, ptr(packed), float(eps), ptr(out))
+    return out
+
+
 def adam(params, grads, exp_avg, exp_avg_sq, *, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt,
          params_bf16=None):
     _lib.call("octsam_adam", ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), params.numel(), beta1, beta2,

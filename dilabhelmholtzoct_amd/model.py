@@ -198,8 +198,9 @@ class VisionEncoder(nn.Module):
 
 
 class MaskEmbedding(nn.Module):
-    """SamMaskEmbedding parameters (hf:modeling_sam.py:569-598); mask prompts are not used by the
-    reference (input_masks is never passed) and are rejected by this implementation."""
+    """SamMaskEmbedding (hf:modeling_sam.py:569-598): the dense prompt of input_masks, one HIP kernel
+    (octsam_mask_embed). The reference never passes input_masks; this is the SamModel surface, forward only
+    (the prompt encoder is frozen on the training path)."""
 
     def __init__(self, cfg):
         super().__init__()
@@ -209,6 +210,30 @@ class MaskEmbedding(nn.Module):
         self.conv3 = nn.Conv2d(c, cfg.hidden_size, kernel_size=1)
         self.layer_norm1 = nn.LayerNorm(c // 4, eps=1e-6)
         self.layer_norm2 = nn.LayerNorm(c, eps=1e-6)
+        self.eps = cfg.layer_norm_eps
+
+    @torch.no_grad()
+    def packed(self) -> torch.Tensor:
+        ps = [self.conv1.weight, self.conv1.bias, self.layer_norm1.weight, self.layer_norm1.bias, self.conv2.weight,
+              self.conv2.bias, self.layer_norm2.weight, self.layer_norm2.bias, self.conv3.weight, self.conv3.bias]
+        return torch.cat([p.detach().reshape(-1).float() for p in ps]).contiguous()
+
+    @torch.no_grad()
+    def forward_pixels(self, masks: torch.Tensor) -> torch.Tensor:
+        """masks [B, 1, 256, 256] (or [B, 256, 256]) -> dense embeddings fp32 [B, 4096, 256] (pixel-major)."""
+        if masks.dim() == 4 and masks.shape[1] == 1:
+            masks = masks[:, 0]
+        if masks.dim() != 3 or tuple(masks.shape[1:]) != (256, 256):
+            raise ValueError(f"input_masks must be [batch_size, 1, 256, 256], got {tuple(masks.shape)}")
+        if self.conv1.out_channels != 4 or self.conv2.out_channels != 16 or self.conv3.out_channels != 256:
+            raise NotImplementedError("mask embedding kernel is built for mask_input_channels 16, hidden 256")
+        m = masks.to(self.conv1.weight.device, torch.float32).contiguous()
+        out = torch.empty(m.shape[0], 4096, 256, device=m.device, dtype=torch.float32)
+        return K.mask_embed(m, self.packed(), self.eps, out)
+
+    def forward(self, masks: torch.Tensor) -> torch.Tensor:
+        """[B, 256, 64, 64] like hf SamMaskEmbedding.forward."""
+        return self.forward_pixels(masks).view(-1, 64, 64, 256).permute(0, 3, 1, 2)
 
 
 class PromptEncoder(nn.Module):
@@ -406,22 +431,31 @@ class SamModel(nn.Module):
         if input_points is not None and input_boxes is not None and input_points.shape[1] != input_boxes.shape[1]:
             raise ValueError("You should provide as many bounding boxes as input points per box. Got "
                              f"{input_points.shape[1]} and {input_boxes.shape[1]}.")
-        if input_masks is not None or attention_similarity is not None or target_embedding is not None:
-            raise NotImplementedError("mask prompts / attention_similarity / target_embedding are not on the "
-                                      "reference's training path and are not implemented")
-        if input_points is None and input_boxes is None:
-            raise NotImplementedError("prompt-free decoding is not on the reference's training path")
+        if attention_similarity is not None or target_embedding is not None:
+            raise NotImplementedError("attention_similarity / target_embedding are not on the reference's "
+                                      "training path and are not implemented")
         if pixel_values is not None:
             emb = self.vision_encoder.forward_nhwc(pixel_values)
         else:
             B_, C_, H_, W_ = image_embeddings.shape
             emb = image_embeddings.permute(0, 2, 3, 1).reshape(B_, H_ * W_, C_).float().contiguous()
-        tokens = self.prompt_tokens(input_points, input_labels, input_boxes)
+        if input_points is None and input_boxes is None:
+            # prompt-free decoding (hf SamPromptEncoder: no sparse embeddings, SamMaskDecoder: the 5 output tokens
+            # alone, point batch 1): every image gets the iou / mask tokens only
+            md = self.mask_decoder
+            tokens = md.output_tokens_f32().reshape(1, 1, 5, 256).expand(emb.shape[0], 1, 5, 256).contiguous()
+        else:
+            tokens = self.prompt_tokens(input_points, input_labels, input_boxes)
         B, N = tokens.shape[:2]
         if emb.shape[0] != B:
             raise ValueError("The batch size of the image embeddings and the input points must be the same. ")
-        masks, iou = self.mask_decoder.run(emb, self.image_pe(), tokens,
-                                           self.prompt_encoder.no_mask_embed.weight, multimask_output)
+        if input_masks is not None:
+            dense = self.prompt_encoder.mask_embed.forward_pixels(input_masks)  # [B, 4096, 256]
+            if dense.shape[0] != B:
+                raise ValueError("input_masks must have one mask per image")
+        else:
+            dense = self.prompt_encoder.no_mask_embed.weight
+        masks, iou = self.mask_decoder.run(emb, self.image_pe(), tokens, dense, multimask_output)
         return SamImageSegmentationOutput(iou_scores=iou, pred_masks=masks)
 
 

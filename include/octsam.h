@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 16
+#define OCTSAM_ABI_VERSION 17
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -199,6 +199,12 @@ int octsam_prompt_tokens(const float* boxes, const float* points, const int32_t*
                          int32_t points_per_prompt, const float* pos_gauss, const float* point_embed,
                          const float* not_a_point, const float* out_tokens, float input_size, float* tokens,
                          void* stream);
+/* SamMaskEmbedding.forward (hf:modeling_sam.py:569-592: the dense prompt of SamModel's input_masks): masks fp32
+ * [B, 256, 256] -> out fp32 [B, 4096, 256] (pixel-major, the decoder's image-embedding layout). packed_weights fp32:
+ * conv1 w [4][4] (out, ky*2+kx), b [4], layer_norm1 w [4], b [4], conv2 w [16][16] (out, in*4 + ky*2 + kx), b [16],
+ * layer_norm2 w [16], b [16], conv3 w [256][16], b [256]; eps = layer_norm_eps. Forward only (the prompt encoder is
+ * frozen on the reference's training path). */
+int octsam_mask_embed(const float* masks, int32_t B, const float* packed_weights, float eps, float* out, void* stream);
 /* SamModel.get_image_wide_positional_embeddings (hf:modeling_sam.py:1128-1139) as [size*size, 256]. */
 int octsam_image_pe(const float* pos_gauss, int32_t size, float* out, void* stream);
 /* dx bf16 [n] = dy fp32 [n] * (y > 0), y bf16 rows of stride ldy with `cols` columns (ReLU backward) */

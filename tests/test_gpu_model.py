@@ -109,3 +109,47 @@ def test_multimask_forward(cuda, models):
         got = ours(image_embeddings=emb, input_boxes=boxes, multimask_output=True)
     assert got.pred_masks.shape == ref.pred_masks.shape == (1, 2, 3, 256, 256)
     assert _rel(got.pred_masks, ref.pred_masks) < 3e-2
+
+
+@pytest.mark.parametrize("multimask", [False, True])
+def test_prompt_free_forward(cuda, models, multimask):
+    """SamModel.forward with no points / boxes (hf: no sparse embeddings, the decoder on its 5 output tokens alone,
+    point batch 1) vs transformers fp32 on the same image embeddings."""
+    ours, hf, _ = models
+    px, _, _ = _inputs(cuda, B=2, N=1, seed=11)
+    with torch.no_grad():
+        emb = hf.vision_encoder(px).last_hidden_state
+        ref = hf(image_embeddings=emb, multimask_output=multimask)
+        got = ours(image_embeddings=emb, multimask_output=multimask)
+    assert got.pred_masks.shape == ref.pred_masks.shape == (2, 1, 3 if multimask else 1, 256, 256)
+    assert _rel(got.pred_masks, ref.pred_masks) < 3e-2
+    assert _rel(got.iou_scores, ref.iou_scores) < 3e-2
+
+
+def test_mask_embedding(cuda, models):
+    """SamMaskEmbedding (octsam_mask_embed) vs transformers fp32 on random mask logits, and a mask prompt through
+    SamModel.forward (dense = mask embedding instead of no_mask_embed) vs transformers."""
+    ours, hf, _ = models
+    g = torch.Generator().manual_seed(5)
+    masks = (torch.randn(2, 1, 256, 256, generator=g) * 4).to(cuda)
+    with torch.no_grad():  # non-trivial biases / LayerNorm affines (only the mask tests read these weights)
+        for (n, p), (n2, p2) in zip(ours.prompt_encoder.mask_embed.named_parameters(),
+                                    hf.prompt_encoder.mask_embed.named_parameters()):
+            assert n == n2
+            v = torch.randn(p.shape, generator=g) * (0.3 if "conv" in n and n.endswith("weight") else 0.5)
+            if "layer_norm" in n and n.endswith("weight"):
+                v = v + 1.0
+            p.copy_(v.to(cuda))
+            p2.copy_(v.to(cuda))
+    with torch.no_grad():
+        ref = hf.prompt_encoder.mask_embed(masks)
+        got = ours.prompt_encoder.mask_embed(masks)
+    assert got.shape == ref.shape == (2, 256, 64, 64)
+    assert _rel(got, ref) < 1e-4
+    px, boxes, _ = _inputs(cuda, B=2, N=1, seed=12)
+    with torch.no_grad():
+        emb = hf.vision_encoder(px).last_hidden_state
+        r = hf(image_embeddings=emb, input_boxes=boxes, input_masks=masks, multimask_output=False)
+        o = ours(image_embeddings=emb, input_boxes=boxes, input_masks=masks, multimask_output=False)
+    assert _rel(o.pred_masks, r.pred_masks) < 3e-2
+    assert _rel(o.iou_scores, r.iou_scores) < 3e-2
