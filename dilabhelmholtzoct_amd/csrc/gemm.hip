@@ -105,11 +105,23 @@ struct GemmK {
   int c_rows;    // rows of C (and R) when a row map scatters the output (fast epilogue range)
   float* a_cs;   // k-major operands: per-batch column sums of A [batch][M] / B [batch][N] (or null)
   float* b_cs;
+  int rgroup;    // broadcast-residual tile order (rgroup_tm); 0 = plain order
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
 __device__ __forceinline__ long long remap(int row, int blk, int rep) {
   return blk > 0 ? (long long)(row / (blk * rep)) * blk + row % blk : (long long)row;
+}
+
+// Row-tile order for a row-remapped broadcast residual (r_blk % 256 == 0, rgroup set): the 256-row tiles that
+// read the same residual rows (same row % r_blk inside one r_blk * r_rep group — the decoder's per-prompt tiles at
+// one positional block) get consecutive logical ids, so the tiles in flight on an XCD share one residual block in
+// L2 instead of re-fetching the whole period per prompt.
+__device__ __forceinline__ int rgroup_tm(const GemmK& p, int tm) {
+  if (!p.rgroup) return tm;
+  const int nb = p.r_blk >> 8, gsz = nb * p.r_rep;
+  const int g = tm / gsz, j = tm - g * gsz;
+  return g * gsz + (j % p.r_rep) * nb + j / p.r_rep;
 }
 
 __device__ __forceinline__ int lds_idx(int r, int c) {  // e16 element index in a [rows][64] image
@@ -1894,7 +1906,7 @@ __global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
   const int per_batch = p.tiles_m * p.tiles_n;
   const int bz = bid / per_batch, rem = bid - bz * per_batch;
   const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
-  const int row0 = tm * 256, col0 = tn * 128;
+  const int row0 = rgroup_tm(p, tm) * 256, col0 = tn * 128;
   const e16* A = (const e16*)p.A + bz * p.sA;
   const e16* B = (const e16*)p.B + bz * p.sB;
   const int nk = p.K / g4::KS;
@@ -1942,13 +1954,23 @@ int launch_gemm4w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
 // the lean kinds of the encoder's GEMMs (QKV / MLP1: e16 C; projections: fp32 C + in-place fp32 residual, with
 // or without the window row map) on the two-workgroup kernel: fast path 0 (default) when g_gemm4w, K % 32 == 0
 static int g_gemm4w = 1;
+// the row-remapped broadcast-addend kind (11) on the two-workgroup kernel when N is not a multiple of 256: the
+// decoder's [K | Q' | V] projection of the per-prompt keys (M = P*4096, N = 384, K = 256) fills 256x128 tiles
+// exactly where 256x256 tiles waste a third; 320 -> 284 us, 270 with the rgroup_tm order (scripts/gemm_res_ab.py,
+// profiles/r03/gemm_res_ab.log;
+// the N = 256 shapes and the plain e16 residual kind 3 measured equal or slower there and stay on the 8-phase
+// kernels); fast path bit 1024 turns it off (A/B)
+static int g_gemm4w_res = 1;
+static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off: A/B)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
     case 1: return launch_gemm4w_fe<EPI, 1>(k, a, s);
     case 2: return launch_gemm4w_fe<EPI, 2>(k, a, s);
+    case 3: return launch_gemm4w_fe<EPI, 3>(k, a, s);
     case 4: return launch_gemm4w_fe<EPI, 4>(k, a, s);
     case 8: return launch_gemm4w_fe<EPI, 8>(k, a, s);
+    case 11: return launch_gemm4w_fe<EPI, 11>(k, a, s);
     default: return -1;
   }
 }
@@ -2021,7 +2043,7 @@ __device__ __forceinline__ Cursor tile_cursor(const GemmK& p, int i, int first, 
   Cursor c;
   c.A = (const e16*)p.A + bz * p.sA;
   c.B = (const e16*)p.B + bz * p.sB;
-  c.row0 = tm * 256;
+  c.row0 = rgroup_tm(p, tm) * 256;
   c.col0 = tn * 256;
   c.i = i;
   c.kt = 0;
@@ -2311,6 +2333,8 @@ int& last_path() { static thread_local int v = 0; return v; }
 extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_small = (enable & 256) ? 0 : 1;
   g_gemm4w = (enable & 512) ? 0 : 1;
+  g_gemm4w_res = (enable & 1024) ? 0 : 1;
+  g_rgroup = (enable & 2048) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2356,6 +2380,11 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   k.alpha = a->alpha; k.beta = a->beta; k.act = a->act;
   k.c_f32 = a->c_f32; k.r_f32 = a->r_f32; k.pre_f32 = a->pre_f32; k.conv_c = a->conv_c;
   k.k_total = a->k_total;
+  // broadcast-residual tile order: whole 256-row tiles per residual period, whole groups of tiles
+  k.rgroup = (g_rgroup && a->R && a->r_blk > 0 && (a->r_blk & 255) == 0 && k.r_rep > 1 && a->row_map == nullptr &&
+              ((a->M + 255) / 256) % ((a->r_blk >> 8) * k.r_rep) == 0)
+                 ? 1
+                 : 0;
   k.a_cs = a->a_colsum;
   k.b_cs = a->b_colsum;
   const bool want_cs = a->a_colsum != nullptr || a->b_colsum != nullptr;
@@ -2438,7 +2467,9 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // 184 -> 195 us, where the 8-phase interleave of one 256x256 workgroup keeps the matrix pipes busier)
       if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->K <= 1024 && a->N <= 1024 &&
           a->batch == 1 && am == 0 && bm == 0 &&
-          a->M >= 4096 && (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
+          a->M >= 4096 &&
+          (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8 ||
+           (g_gemm4w_res && k.fast_epi == 11 && a->K <= 512 && a->N % 256 != 0)) &&
           (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 40)) {
         t_last_path = 2;
         if (a->act == OCTSAM_ACT_GELU) return launch_gemm4w<OCTSAM_ACT_GELU>(k, a, s);

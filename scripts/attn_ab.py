@@ -54,4 +54,5 @@ for i, (side, nseq, heads, hd, dt, qkv, outs, *_) in enumerate(data):
         row[f"v{v}_us"] = round(best[i, v], 1)
         row[f"v{v}_tf"] = round(fl / best[i, v] / 1e6, 1)
         row[f"v{v}_same"] = bool(torch.equal(outs[v], ref))
+        row[f"v{v}_rel"] = float((outs[v].float() - ref.float()).norm() / ref.float().norm())
     print(json.dumps(row), flush=True)

@@ -601,3 +601,30 @@ def test_wgrad_tok(cuda, M, O, I, ldy_pad, ldx_pad, db, beta):
     again = out0.clone()
     kernels.wgrad_tok(dy, x, M, again, ldy=ldy, ldx=ldx, beta=beta)
     assert torch.equal(again, out)
+
+
+@pytest.mark.parametrize("N", [384, 640])
+def test_gemm4w_broadcast_residual(cuda, N):
+    """The row-remapped broadcast-addend kind (the decoder's [K | Q' | V] projection of the per-prompt keys plus the
+    positional projection) on the two-workgroup 256x128 kernel (N not a multiple of 256) against torch fp32 and
+    bit-identical to the persistent 8-phase kernel (fast path bit 1024)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    L, P, K = 4096, 3, 256
+    M = L * P
+    g = torch.Generator().manual_seed(N)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(L, N, generator=g).to(cuda, torch.bfloat16)
+    outs = []
+    for fast in (1, 1 | 1024):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, residual=R, ldr=N, r_remap=(L, P))
+        assert lib.octsam_gemm_last_path() == 2
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    ref = A.float() @ W.float().t() + bias + R.float().repeat(P, 1)
+    assert _rel(outs[0], ref) < 5e-3
+    assert torch.equal(outs[0], outs[1])
