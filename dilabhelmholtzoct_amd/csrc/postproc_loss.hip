@@ -13,6 +13,7 @@
 //   topo     : sigmoid + F.interpolate(->50x50, bilinear, align_corners=True) of the selected pred maps
 //              and of the gt maps (ref:octsam/models/topological_loss.py:33-46), and the scatter of
 //              the diagram-value gradients back through that downsample and the sigmoid.
+#include <cstdlib>
 #include "common.h"
 #include "../../include/octsam.h"
 
@@ -180,6 +181,79 @@ __global__ __launch_bounds__(256) void confusion_kernel(const float* __restrict_
   if (tid < 4)
     atomicAdd(counts + 4 * m + tid,
               (unsigned long long)(red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]));
+}
+
+// dicece_bwd_kernel with four consecutive pixels per thread (HW % 4 == 0, N <= NR): 16-B logit loads and stores,
+// 4-B target loads (the scalar form's 1-B loads move a quarter of the bytes per wave instruction). The same
+// per-element arithmetic in the same order (dmask agrees with the scalar form to the last bits the compiler's FMA
+// contraction moves): 200 -> 124 us at B = 8, N = 21, 496 x 512 (scripts/dicece_ab.py, profiles/r03/dicece_ab.log).
+template <int NR>
+__global__ __launch_bounds__(256) void dicece_bwd4_kernel(const float* __restrict__ x, const uint8_t* __restrict__ gt,
+                                                          const float* __restrict__ coef, int B, int N, int HW,
+                                                          float w_dice, float w_ce, float inv_bhw,
+                                                          float* __restrict__ dx, double* __restrict__ ce_part) {
+  const int q4 = HW >> 2, total = B * q4;  // host-checked: B * HW < 2^31
+  double ce = 0.0;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int b = e / q4, pix = (e - b * q4) * 4;
+    const long long o0 = (long long)b * N * HW + pix;
+    const float* cfb = coef + 2 * b * N;
+    float4 xv[NR];
+    uint32_t tv[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      if (n < N) {
+        xv[n] = *(const float4*)(x + o0 + (long long)n * HW);
+        tv[n] = *(const uint32_t*)(gt + o0 + (long long)n * HW);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        if (n < N) mx = fmaxf(mx, ((const float*)&xv[n])[k]);
+      float se = 0.0f, tsum = 0.0f, tx = 0.0f;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          const float xk = ((const float*)&xv[n])[k], tk = (float)((tv[n] >> (8 * k)) & 0xFF);
+          se += __expf(xk - mx);
+          tsum += tk;
+          tx += tk * xk;
+        }
+      }
+      const float lse = mx + __logf(se);
+      ce += (double)(lse * tsum - tx);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          const float xk = ((const float*)&xv[n])[k], tk = (float)((tv[n] >> (8 * k)) & 0xFF);
+          const float sm = __expf(xk - lse);
+          const float p = 1.0f / (1.0f + __expf(-xk));
+          const float gd = (cfb[2 * n] * tk + cfb[2 * n + 1]) * p * (1.0f - p);
+          const float gc = (sm * tsum - tk) * inv_bhw;
+          ((float*)&xv[n])[k] = w_dice * gd + w_ce * gc;  // the logit is dead: its register takes d
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n)
+      if (n < N) *(float4*)(dx + o0 + (long long)n * HW) = xv[n];
+  }
+  __shared__ double red[4];
+  ce = wave_sum_d(ce);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ce;
+  __syncthreads();
+  if (threadIdx.x == 0) ce_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+// A/B: OCTSAM_DICECE_SCALAR=1 in the environment keeps the scalar kernel
+bool dicece_vec_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("OCTSAM_DICECE_SCALAR");
+    return !(v && v[0] == '1');
+  }();
+  return on;
 }
 
 // per-map dice sums -> dice loss per map, and the per-map gradient coefficients
@@ -469,7 +543,12 @@ extern "C" int octsam_dicece_bwd(const float* masks, const uint8_t* gt, const fl
   OCTSAM_CHECK_ARG((long long)B * HW < (1LL << 31), "octsam_dicece_bwd: B*HW too large");
   const float inv = (float)(1.0 / ((double)B * HW));
   hipStream_t s = (hipStream_t)stream;
-  if (N <= 32)
+  const bool vec = dicece_vec_enabled() && HW % 4 == 0 && ((uintptr_t)masks & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
+                   ((uintptr_t)gt & 3) == 0;
+  if (vec && N <= 24)
+    hipLaunchKernelGGL(dicece_bwd4_kernel<24>, dim3(nblk), dim3(256), 0, s, masks, gt, coef, B, N, (int)HW, w_dice,
+                       w_ce, inv, dmask, ce_part);
+  else if (N <= 32)
     hipLaunchKernelGGL(dicece_bwd_kernel<32>, dim3(nblk), dim3(256), 0, s, masks, gt, coef, B, N, (int)HW, w_dice, w_ce,
                        inv, dmask, ce_part);
   else
