@@ -3,7 +3,9 @@
 wgrad_off = image-side weight gradients by the split-K tile GEMM, tok_off = token-side ones by the split-K tile
 GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence forked beside
 the DiceCE backward too, ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
-the mask-head backward). Interleaved rounds, median of 5 rounds x 20 steps. Diagnostic only."""
+the mask-head backward, g4res_off = the decoder's [K | Q' | V] projection on the persistent 8-phase GEMM in plain tile
+order, octsam_gemm fast path 1 | 1024 | 2048, while capturing). Interleaved rounds, median of 5 rounds x 20 steps.
+Diagnostic only."""
 import json
 import os
 import statistics
@@ -16,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd import _lib, data
     from dilabhelmholtzoct_amd.model import SamModel
     from dilabhelmholtzoct_amd.train import FusedTrainStep
     dev = torch.device("cuda", 0)
@@ -28,7 +30,10 @@ def main():
     dec = model.mask_decoder
     # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
     VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
-                "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False})}
+                "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
+                "g4res_off": ({}, {})}
+    FAST = {"g4res_off": 1 | 1024 | 2048}
+    lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
         st_attr, dec_attr = VARIANTS[name]
         st = FusedTrainStep(model, lr=1e-3, topological=True, graphs=True,
@@ -38,9 +43,11 @@ def main():
         saved = {k: getattr(dec, k) for k in dec_attr}
         for k, v in dec_attr.items():
             setattr(dec, k, v)
+        lib.octsam_gemm_set_fast_path(FAST.get(name, 1))
         for i in range(3):  # capture + warm
             st.step(batch, next_batch=batch if i < 2 else None)
         st.flush()
+        lib.octsam_gemm_set_fast_path(1)
         for k, v in saved.items():
             setattr(dec, k, v)
         variants[name] = st
