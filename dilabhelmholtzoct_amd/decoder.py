@@ -231,10 +231,13 @@ class MaskDecoder(nn.Module):
         return self._group(self.flat, ["iou_token.weight", "mask_tokens.weight"], 0)
 
     # ------------------------------------------------------------------ forward entry
-    def run(self, emb, pe, tokens, no_mask_weight, multimask_output: bool):
+    def run(self, emb, pe, tokens, no_mask_weight, multimask_output: bool, target_embedding=None):
         """emb fp32 [B, 4096, 256]; pe fp32 [4096, 256]; tokens fp32 [B, N, T, 256] ->
-        (pred_masks [B, N, k, 256, 256], iou_scores [B, N, k])."""
-        return MaskDecoderFn.apply(self.flat, emb, pe, tokens, no_mask_weight.detach(), self, bool(multimask_output))
+        (pred_masks [B, N, k, 256, 256], iou_scores [B, N, k]). target_embedding: broadcastable to the tokens
+        (hf SamTwoWayTransformer's PerSAM hook)."""
+        tgt = None if target_embedding is None else target_embedding.detach()
+        return MaskDecoderFn.apply(self.flat, emb, pe, tokens, no_mask_weight.detach(), self, bool(multimask_output),
+                                   tgt)
 
     # ------------------------------------------------------------------ helpers
     def _lin(self, x, wname, bname, out, M, *, act=0, residual=None, r_remap=(0, 1), a_mode=0, A2=None,
@@ -431,7 +434,7 @@ class MaskDecoder(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
-    def forward_impl(self, emb, pe, tokens, no_mask, multimask):
+    def forward_impl(self, emb, pe, tokens, no_mask, multimask, target=None):
         cfg = self.config
         B, N, T, _ = tokens.shape
         P, R = B * N, B * N * T
@@ -444,6 +447,15 @@ class MaskDecoder(nn.Module):
         tr = "transformer."
 
         tok0 = tokens.reshape(R, C).contiguous()
+        tgt = None
+        if target is not None:
+            # hf SamTwoWayTransformer: `queries += target_embedding` before every layer; the first add is in place
+            # on point_embeddings itself, so the query positional embedding of every layer (and of the final
+            # attention) is tokens + target as well
+            tgt = target.to(device=dev, dtype=torch.float32).expand(B, N, T, C).reshape(R, C).contiguous()
+            t0 = torch.empty_like(tok0)
+            K.axpby(tok0, tgt, t0)
+            tok0 = t0
         s.tok0 = tok0
         s.tok0_b = self._bf(tok0)
         imgd = torch.empty(B * L, C, device=dev, dtype=f32)
@@ -464,6 +476,10 @@ class MaskDecoder(nn.Module):
             pre = tr + f"layers.{li}."
             sa, t2i, i2t = pre + "self_attn.", pre + "cross_attn_token_to_image.", pre + "cross_attn_image_to_token."
             ls = SimpleNamespace()
+            if tgt is not None and li > 0:  # queries += target_embedding (layer 0: folded into tok0 above)
+                qn, qb = torch.empty_like(queries), torch.empty(R, C, device=dev, dtype=b16)
+                K.axpby(queries, tgt, qb, out2_f32=qn)
+                queries, queries_b = qn, qb
             # ---- self attention (layer 0: skip_first_layer_pe -> no residual, no PE; :313-321)
             if li == 0:
                 qin_b = s.tok0_b
@@ -771,8 +787,8 @@ class MaskDecoderFn(torch.autograd.Function):
     image/prompt tensors); grad = flat gradient buffer."""
 
     @staticmethod
-    def forward(ctx, flat, emb, pe, tokens, no_mask, dec: MaskDecoder, multimask: bool):
-        masks, iou, saved = dec.forward_impl(emb, pe, tokens, no_mask, multimask)
+    def forward(ctx, flat, emb, pe, tokens, no_mask, dec: MaskDecoder, multimask: bool, target=None):
+        masks, iou, saved = dec.forward_impl(emb, pe, tokens, no_mask, multimask, target)
         ctx.saved = saved
         ctx.dec = dec
         ctx.mark_non_differentiable(iou)
@@ -783,4 +799,4 @@ class MaskDecoderFn(torch.autograd.Function):
         dec = ctx.dec
         g = dec.backward_impl(ctx.saved, dmasks)
         ctx.saved = None
-        return g, None, None, None, None, None, None
+        return g, None, None, None, None, None, None, None

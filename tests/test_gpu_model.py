@@ -153,3 +153,21 @@ def test_mask_embedding(cuda, models):
         o = ours(image_embeddings=emb, input_boxes=boxes, input_masks=masks, multimask_output=False)
     assert _rel(o.pred_masks, r.pred_masks) < 3e-2
     assert _rel(o.iou_scores, r.iou_scores) < 3e-2
+
+
+def test_target_embedding(cuda, models):
+    """SamModel.forward(target_embedding=...) — hf SamTwoWayTransformer's `queries += target_embedding` before every
+    layer, whose first add lands in place on the point embeddings (so every query positional embedding carries it
+    too) — vs transformers fp32 on the same image embeddings and boxes."""
+    ours, hf, _ = models
+    px, boxes, _ = _inputs(cuda, B=2, N=2, seed=13)
+    g = torch.Generator().manual_seed(14)
+    tgt = (torch.randn(2, 1, 1, 256, generator=g) * 0.5).to(cuda)
+    with torch.no_grad():
+        emb = hf.vision_encoder(px).last_hidden_state
+        r = hf(image_embeddings=emb, input_boxes=boxes, target_embedding=tgt.clone(), multimask_output=True)
+        o = ours(image_embeddings=emb, input_boxes=boxes, target_embedding=tgt, multimask_output=True)
+        plain = ours(image_embeddings=emb, input_boxes=boxes, multimask_output=True)
+    assert _rel(o.pred_masks, r.pred_masks) < 3e-2
+    assert _rel(o.iou_scores, r.iou_scores) < 3e-2
+    assert _rel(plain.pred_masks, r.pred_masks) > 0.1  # the hook changes the result
