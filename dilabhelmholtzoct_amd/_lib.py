@@ -94,6 +94,8 @@ _SIGNATURES = {
     "octsam_dec_t2i_workspace": (c_int64, [c_int32, c_int32]),
     "octsam_dec_t2i_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_dec_t2i_fwd_bias": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_dec_t2i_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                      c_void_p, c_void_p]),

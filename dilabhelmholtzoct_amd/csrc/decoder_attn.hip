@@ -229,10 +229,13 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 }  // namespace t2
 
-// q fp32 [P,Tq,128]; k, v bf16 rows [(p / kv_rep) * L + key] * ldkv; part fp32 [P][nchunk][4][PART]
+// q fp32 [P,Tq,128]; k, v bf16 rows [(p / kv_rep) * L + key] * ldkv; part fp32 [P][nchunk][4][PART];
+// sbias (or null): fp32 [P][L] added to every head's and token's logits of key (hf SamAttention's
+// attention_similarity mask, natural-log units)
 __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
                                                       const bf16* __restrict__ v, long long ldkv, int kv_rep, int Tq,
-                                                      int L, int nchunk, float* __restrict__ part) {
+                                                      int L, int nchunk, float* __restrict__ part,
+                                                      const float* __restrict__ sbias) {
   using namespace t2;
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6;
@@ -262,6 +265,15 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
       const bf16x8 kf = row_op(slot, t, false, lane);
       st[t] = mfma32(kf, qhi, (f32x4)0.0f);
       st[t] = mfma32(kf, qlo, st[t]);
+    }
+    if (sbias) {  // S^T[key 16t + 4g + i][token c] += bias[key] (log2 units like the scores)
+      const float* bp = sbias + (long long)p * L + key0 + s * STEP + 4 * (lane >> 4);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 bv = *(const f32x4*)(bp + 16 * t);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[t][i] = fmaf(bv[i], L2E, st[t][i]);
+      }
     }
     float mx = fmaxf(fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3])),
                      fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
@@ -620,21 +632,27 @@ static void t2i_smem_attr() {
   }
 }
 
-extern "C" int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
-                                  int32_t Tq, int32_t L, void* out, float* lse, float* workspace, void* stream) {
+extern "C" int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
+                                       int32_t P, int32_t Tq, int32_t L, const float* score_bias, void* out, float* lse,
+                                       float* workspace, void* stream) {
   OCTSAM_CHECK_ARG(q && k && v && out && lse && workspace && P > 0 && Tq > 0 && Tq <= MAXT && L > 0 && L % 32 == 0 &&
                        kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 && (uintptr_t)k % 16 == 0 &&
-                       (uintptr_t)v % 16 == 0,
+                       (uintptr_t)v % 16 == 0 && (uintptr_t)score_bias % 16 == 0,
                    "octsam_dec_t2i_fwd: bad args");
   t2i_smem_attr();
   const int nch = t2i_nchunk(L);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(t2i_fwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, s, q, (const bf16*)k, (const bf16*)v, ldkv,
-                     kv_rep, Tq, L, nch, workspace);
+                     kv_rep, Tq, L, nch, workspace, score_bias);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
   hipLaunchKernelGGL(t2i_combine_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)out, lse);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
   return 0;
+}
+
+extern "C" int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                                  int32_t Tq, int32_t L, void* out, float* lse, float* workspace, void* stream) {
+  return octsam_dec_t2i_fwd_bias(q, k, v, ldkv, kv_rep, P, Tq, L, nullptr, out, lse, workspace, stream);
 }
 
 extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,

@@ -231,13 +231,16 @@ class MaskDecoder(nn.Module):
         return self._group(self.flat, ["iou_token.weight", "mask_tokens.weight"], 0)
 
     # ------------------------------------------------------------------ forward entry
-    def run(self, emb, pe, tokens, no_mask_weight, multimask_output: bool, target_embedding=None):
+    def run(self, emb, pe, tokens, no_mask_weight, multimask_output: bool, target_embedding=None,
+            attention_similarity=None):
         """emb fp32 [B, 4096, 256]; pe fp32 [4096, 256]; tokens fp32 [B, N, T, 256] ->
-        (pred_masks [B, N, k, 256, 256], iou_scores [B, N, k]). target_embedding: broadcastable to the tokens
-        (hf SamTwoWayTransformer's PerSAM hook)."""
+        (pred_masks [B, N, k, 256, 256], iou_scores [B, N, k]). target_embedding: broadcastable to the tokens;
+        attention_similarity: broadcastable to [B*N, 1, 1, 4096], added to the token->image logits of the two
+        transformer layers (hf's PerSAM hooks; forward only)."""
         tgt = None if target_embedding is None else target_embedding.detach()
+        sim = None if attention_similarity is None else attention_similarity.detach()
         return MaskDecoderFn.apply(self.flat, emb, pe, tokens, no_mask_weight.detach(), self, bool(multimask_output),
-                                   tgt)
+                                   tgt, sim)
 
     # ------------------------------------------------------------------ helpers
     def _lin(self, x, wname, bname, out, M, *, act=0, residual=None, r_remap=(0, 1), a_mode=0, A2=None,
@@ -434,7 +437,7 @@ class MaskDecoder(nn.Module):
         return out
 
     # ------------------------------------------------------------------ forward
-    def forward_impl(self, emb, pe, tokens, no_mask, multimask, target=None):
+    def forward_impl(self, emb, pe, tokens, no_mask, multimask, target=None, similarity=None):
         cfg = self.config
         B, N, T, _ = tokens.shape
         P, R = B * N, B * N * T
@@ -457,6 +460,14 @@ class MaskDecoder(nn.Module):
             K.axpby(tok0, tgt, t0)
             tok0 = t0
         s.tok0 = tok0
+        sbias = None
+        if similarity is not None:
+            sim = similarity.to(device=dev, dtype=torch.float32)
+            if sim.dim() != 4 or sim.shape[1] != 1 or sim.shape[2] != 1 or sim.shape[3] != L or sim.shape[0] not in (1, P):
+                raise ValueError(f"attention_similarity must broadcast as [B*N, 1, 1, {L}] (heads and tokens "
+                                 f"shared), got {tuple(sim.shape)}")
+            sbias = sim.reshape(-1, L).expand(P, L).contiguous()
+        s.similarity = sbias is not None
         s.tok0_b = self._bf(tok0)
         imgd = torch.empty(B * L, C, device=dev, dtype=f32)
         imgd_b = torch.empty(B * L, C, device=dev, dtype=b16)
@@ -513,7 +524,7 @@ class MaskDecoder(nn.Module):
             ls.KQV, ls.kv_src_b, ls.kv_rep = KQV, src_b, kv_rep
             to_b = torch.empty(R, CI, device=dev, dtype=b16)
             lse = torch.empty(P, 8, T, device=dev, dtype=f32)
-            K.t2i_fwd(Q, KQV, KQV[:, 2 * CI:], 3 * CI, kv_rep, P, T, L, to_b, lse)
+            K.t2i_fwd(Q, KQV, KQV[:, 2 * CI:], 3 * CI, kv_rep, P, T, L, to_b, lse, score_bias=sbias)
             ls.t2i_Q, ls.t2i_o_b, ls.t2i_lse = Q, to_b, lse
             s2 = self._lin(to_b, t2i + "out_proj.weight", t2i + "out_proj.bias",
                            torch.empty(R, C, device=dev, dtype=f32), R, residual=queries)
@@ -787,8 +798,8 @@ class MaskDecoderFn(torch.autograd.Function):
     image/prompt tensors); grad = flat gradient buffer."""
 
     @staticmethod
-    def forward(ctx, flat, emb, pe, tokens, no_mask, dec: MaskDecoder, multimask: bool, target=None):
-        masks, iou, saved = dec.forward_impl(emb, pe, tokens, no_mask, multimask, target)
+    def forward(ctx, flat, emb, pe, tokens, no_mask, dec: MaskDecoder, multimask: bool, target=None, similarity=None):
+        masks, iou, saved = dec.forward_impl(emb, pe, tokens, no_mask, multimask, target, similarity)
         ctx.saved = saved
         ctx.dec = dec
         ctx.mark_non_differentiable(iou)
@@ -797,6 +808,8 @@ class MaskDecoderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dmasks, diou):
         dec = ctx.dec
+        if getattr(ctx.saved, "similarity", False):
+            raise NotImplementedError("attention_similarity is a forward-only (inference) hook")
         g = dec.backward_impl(ctx.saved, dmasks)
         ctx.saved = None
-        return g, None, None, None, None, None, None, None
+        return g, None, None, None, None, None, None, None, None

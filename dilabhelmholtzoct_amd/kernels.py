@@ -304,10 +304,17 @@ def _t2i_workspace(P, L, device):
     return torch.empty(n, device=device, dtype=torch.float32)
 
 
-def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse):
+def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse, score_bias=None):
+    """score_bias: fp32 [P, L] added to the logits (attention_similarity), or None."""
     _require_cuda(q, k, v, out, lse)
     ws = _t2i_workspace(P, L, q.device)
-    _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse), ptr(ws))
+    if score_bias is None:
+        _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse), ptr(ws))
+    else:
+        if score_bias.dtype != torch.float32 or score_bias.numel() != P * L or not score_bias.is_contiguous():
+            raise ValueError("t2i_fwd: score_bias must be contiguous fp32 [P, L]")
+        _lib.call("octsam_dec_t2i_fwd_bias", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(score_bias),
+                  ptr(out), ptr(lse), ptr(ws))
 
 
 def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):

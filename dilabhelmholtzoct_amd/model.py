@@ -431,9 +431,6 @@ class SamModel(nn.Module):
         if input_points is not None and input_boxes is not None and input_points.shape[1] != input_boxes.shape[1]:
             raise ValueError("You should provide as many bounding boxes as input points per box. Got "
                              f"{input_points.shape[1]} and {input_boxes.shape[1]}.")
-        if attention_similarity is not None:
-            raise NotImplementedError("attention_similarity (a PerSAM inference hook the reference never passes) is "
-                                      "not implemented")
         if pixel_values is not None:
             emb = self.vision_encoder.forward_nhwc(pixel_values)
         else:
@@ -456,7 +453,8 @@ class SamModel(nn.Module):
         else:
             dense = self.prompt_encoder.no_mask_embed.weight
         masks, iou = self.mask_decoder.run(emb, self.image_pe(), tokens, dense, multimask_output,
-                                           target_embedding=target_embedding)
+                                           target_embedding=target_embedding,
+                                           attention_similarity=attention_similarity)
         return SamImageSegmentationOutput(iou_scores=iou, pred_masks=masks)
 
 

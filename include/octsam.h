@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 17
+#define OCTSAM_ABI_VERSION 18
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -269,6 +269,12 @@ int octsam_dec_tok_attn_bwd(const float* q, const float* k, const float* v, cons
 int64_t octsam_dec_t2i_workspace(int32_t P, int32_t L);
 int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
                        int32_t L, void* out, float* lse, float* workspace, void* stream);
+/* octsam_dec_t2i_fwd with score_bias fp32 [P][L] (16-B aligned, or null) added to every head's and token's logits
+ * of each key: SamAttention's attention_similarity mask (hf:modeling_sam.py SamTwoWayAttentionBlock, the PerSAM
+ * hook), forward only. */
+int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                            int32_t Tq, int32_t L, const float* score_bias, void* out, float* lse, float* workspace,
+                            void* stream);
 int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
                        int32_t L, const void* out, const float* dout, const float* lse, void* dq, void* dk, void* dv,
                        int64_t lddkv, float* workspace, void* stream);

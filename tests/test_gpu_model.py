@@ -171,3 +171,28 @@ def test_target_embedding(cuda, models):
     assert _rel(o.pred_masks, r.pred_masks) < 3e-2
     assert _rel(o.iou_scores, r.iou_scores) < 3e-2
     assert _rel(plain.pred_masks, r.pred_masks) > 0.1  # the hook changes the result
+
+
+@pytest.mark.parametrize("per_prompt", [False, True])
+def test_attention_similarity(cuda, models, per_prompt):
+    """SamModel.forward(attention_similarity=...) — added to the token->image attention logits of both two-way
+    layers (hf SamAttention's attention mask, the PerSAM hook), shared [1, 1, 1, 4096] or per prompt
+    [B*N, 1, 1, 4096] — vs transformers fp32; training through it is refused."""
+    ours, hf, _ = models
+    px, boxes, _ = _inputs(cuda, B=2, N=2, seed=15)
+    g = torch.Generator().manual_seed(16)
+    sim = (torch.randn(4 if per_prompt else 1, 1, 1, 4096, generator=g) * 8.0).to(cuda)
+    with torch.no_grad():
+        emb = hf.vision_encoder(px).last_hidden_state
+        r = hf(image_embeddings=emb, input_boxes=boxes, attention_similarity=sim, multimask_output=True)
+        r0 = hf(image_embeddings=emb, input_boxes=boxes, multimask_output=True)
+        o = ours(image_embeddings=emb, input_boxes=boxes, attention_similarity=sim, multimask_output=True)
+        o0 = ours(image_embeddings=emb, input_boxes=boxes, multimask_output=True)
+    assert _rel(o.pred_masks, r.pred_masks) < 3e-2
+    assert _rel(o.iou_scores, r.iou_scores) < 3e-2
+    # the hook's own effect (small with the synthetic N(0, 0.02) weights) matches transformers' effect
+    assert _rel(r.pred_masks, r0.pred_masks) > 5e-3
+    assert _rel(o.pred_masks - o0.pred_masks, r.pred_masks - r0.pred_masks) < 0.15
+    out = ours(image_embeddings=emb, input_boxes=boxes, attention_similarity=sim, multimask_output=True)
+    with pytest.raises(NotImplementedError):
+        out.pred_masks.float().sum().backward()
