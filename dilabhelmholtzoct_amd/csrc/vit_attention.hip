@@ -471,11 +471,19 @@ __global__ __launch_bounds__(THR) void vit_attn_global_kernel(const E* __restric
 constexpr int NW4 = 4, THR4 = NW4 * 64;
 constexpr int G4_RELH = NW4 * 64 * 32 * 4;  // rel_h tables [64 kh][32 q] fp32 per wave: 32 KiB
 template <int HD> constexpr int g4_smem() { return G4_RELH + 2 * Geo<HD>::TILE + 128; }
+// HALF: each wave keeps the rel_h rows of 32 key rows at a time ([32 kh][32 q] fp32, 16 KiB for the workgroup; the
+// second half is computed when the loop reaches key row 32), so three workgroups share a CU (the rel_w scratch then
+// sets the size). Same values as the whole table: bit-identical.
+template <int HD> constexpr int g4h_smem() {
+  return (G4_RELH / 2 + 2 * Geo<HD>::TILE + 128) > NW4 * G_SCR * 4 ? (G4_RELH / 2 + 2 * Geo<HD>::TILE + 128)
+                                                                     : NW4 * G_SCR * 4;
+}
+static_assert(3 * g4h_smem<64>() <= 160 * 1024, "three half-table global workgroups per CU at head_dim 64");
 static_assert(2 * g4_smem<80>() <= 160 * 1024, "two 4-wave global workgroups per CU");
 template <> __device__ __forceinline__ void wait_vm<16>() { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); }
 
-template <int HD, typename E>
-__global__ __launch_bounds__(THR4, 2) void vit_attn_global4_kernel(const E* __restrict__ qkv, E* __restrict__ out,
+template <int HD, typename E, bool HALF = false>
+__global__ __launch_bounds__(THR4, HALF ? 3 : 2) void vit_attn_global4_kernel(const E* __restrict__ qkv, E* __restrict__ out,
                                                                    const float* __restrict__ Rh,
                                                                    const float* __restrict__ Rw, int heads, float scale) {
   using G = Geo<HD>;
@@ -510,14 +518,20 @@ __global__ __launch_bounds__(THR4, 2) void vit_attn_global4_kernel(const E* __re
 #pragma unroll
     for (int r = 0; r < 16; ++r) relw[t2][r] = scr[(l32 - (32 * t2 + acc_row(r, h)) + 63) * 33 + l32] * inv_scale;
   __syncthreads();
-  float* relh = (float*)gsm + wave * (64 * 32);
+  float* relh = (float*)gsm + wave * (HALF ? 32 * 32 : 64 * 32);
+  if constexpr (HALF) {  // key rows 0..31 now (table block b = 1), 32..63 at tile 32
+    const f32x16 t = rel_block<HD, E>(Rh, qh + 32, 2 * S - 1, qf, lane);
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const f32x16 t = rel_block<HD, E>(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+    for (int r = 0; r < 16; ++r) relh[(31 - acc_row(r, h)) * 32 + l32] = t[r] * L2E;
+  } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
+    for (int b = 0; b < 2; ++b) {
+      const f32x16 t = rel_block<HD, E>(Rh, qh + 32 * b, 2 * S - 1, qf, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) relh[(63 - (32 * b + acc_row(r, h))) * 32 + l32] = t[r] * L2E;
+    }
   }
-  char* ring = gsm + G4_RELH;
+  char* ring = gsm + (HALF ? G4_RELH / 2 : G4_RELH);
   char* zero = ring + 2 * G::TILE;
   if (tid < 32) ((float*)zero)[tid] = 0.0f;
   __syncthreads();
@@ -539,7 +553,14 @@ __global__ __launch_bounds__(THR4, 2) void vit_attn_global4_kernel(const E* __re
     f32x16 sacc[2];
 #pragma unroll
     for (int t2 = 0; t2 < 2; ++t2) sacc[t2] = qk_block<HD, E>(slot, t2, qf, relw[t2], l32, h);
-    const float rh = relh[tile * 32 + l32];
+    if constexpr (HALF) {
+      if (tile == 32) {  // key rows 32..63 (table block b = 0) over the wave's own rows 0..31 (wave-local)
+        const f32x16 t = rel_block<HD, E>(Rh, qh, 2 * S - 1, qf, lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) relh[(31 - acc_row(r, h)) * 32 + l32] = t[r] * L2E;
+      }
+    }
+    const float rh = relh[(HALF ? (tile & 31) : tile) * 32 + l32];
     float mx = sacc[0][0];
 #pragma unroll
     for (int i = 1; i < 31; i += 2) mx = max3f(mx, sacc[i >> 4][i & 15], sacc[(i + 1) >> 4][(i + 1) & 15]);
@@ -895,8 +916,9 @@ __global__ __launch_bounds__(WTHR, HD == 64 ? 3 : 2) void vit_attn_window_kernel
 }
 
 // global-layer kernel (octsam_attention_set_variant): 0 software-pipelined 8-wave loop, 1 plain 8-wave loop, 2 4-wave
-// workgroups two per CU, -1 (default) 2 for head_dim 64 and 1 for head_dim 80 (same-box A/B, scripts/attn_ab.py,
-// profiles/r03/attn_variant_ab.log: vit-b 522.5 -> 498.6 us, vit-h fp16 929.6 vs 934.3 us; all bit-identical)
+// workgroups two per CU, 6 the same with half rel_h tables three per CU, -1 (default) 6 for head_dim 64 and 1 for
+// head_dim 80 (same-box A/Bs, scripts/attn_ab.py: profiles/r03/attn_variant_ab.log vit-b 522.5 -> 498.6 us (2),
+// vit-h fp16 929.6 vs 934.3 us; profiles/r03/attn_half_table_ab.log vit-b 509.6 -> 483.7 us (6); all bit-identical)
 int g_attn_variant = -1;
 
 template <int HD, typename E>
@@ -905,7 +927,7 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
   const float scale = 1.0f / sqrtf((float)HD);
   if (side == 64) {
     static_assert(4096 / (NW * 32) == 16, "16 query blocks per (sequence, head)");
-    const int variant = g_attn_variant >= 0 ? g_attn_variant : (HD == 64 ? 2 : 1);
+    const int variant = g_attn_variant >= 0 ? g_attn_variant : (HD == 64 ? 6 : 1);
     if (variant == 1) {  // the plain loop (A/B)
       static bool attr = false;
       if (!attr) {
@@ -914,6 +936,15 @@ int launch(const void* qkv, void* out, const float* Rh, const float* Rw, int nse
         attr = true;
       }
       hipLaunchKernelGGL((vit_attn_global_kernel<HD, E>), dim3(16 * heads * nseq), dim3(THR), g_smem<HD>(), s,
+                         (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
+    } else if (variant == 6) {  // 4-wave workgroups with half rel_h tables, three per CU
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vit_attn_global4_kernel<HD, E, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, g4h_smem<HD>());
+        attr = true;
+      }
+      hipLaunchKernelGGL((vit_attn_global4_kernel<HD, E, true>), dim3(32 * heads * nseq), dim3(THR4), g4h_smem<HD>(), s,
                          (const E*)qkv, (E*)out, Rh, Rw, heads, scale);
     } else if (variant == 2) {  // 4-wave workgroups, two per CU
       static bool attr = false;

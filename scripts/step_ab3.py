@@ -4,7 +4,8 @@ wgrad_off = image-side weight gradients by the split-K tile GEMM, tok_off = toke
 GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence forked beside
 the DiceCE backward too, ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
 the mask-head backward, g4res_off = the decoder's [K | Q' | V] projection on the persistent 8-phase GEMM in plain tile
-order, octsam_gemm fast path 1 | 1024 | 2048, while capturing). Interleaved rounds, median of 5 rounds x 20 steps.
+order, octsam_gemm fast path 1 | 1024 | 2048, while capturing; attn_v2 = the global attention with whole rel_h
+tables, two workgroups per CU). Interleaved rounds, median of 5 rounds x 20 steps.
 Diagnostic only."""
 import json
 import os
@@ -31,8 +32,9 @@ def main():
     # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
     VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
                 "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
-                "g4res_off": ({}, {})}
+                "g4res_off": ({}, {}), "attn_v2": ({}, {})}
     FAST = {"g4res_off": 1 | 1024 | 2048}
+    ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
         st_attr, dec_attr = VARIANTS[name]
@@ -44,10 +46,12 @@ def main():
         for k, v in dec_attr.items():
             setattr(dec, k, v)
         lib.octsam_gemm_set_fast_path(FAST.get(name, 1))
+        lib.octsam_attention_set_variant(ATTN.get(name, -1))
         for i in range(3):  # capture + warm
             st.step(batch, next_batch=batch if i < 2 else None)
         st.flush()
         lib.octsam_gemm_set_fast_path(1)
+        lib.octsam_attention_set_variant(-1)
         for k, v in saved.items():
             setattr(dec, k, v)
         variants[name] = st
