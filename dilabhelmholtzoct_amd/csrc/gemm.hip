@@ -1959,7 +1959,9 @@ static int g_gemm4w = 1;
 // exactly where 256x256 tiles waste a third; 320 -> 284 us, 270 with the rgroup_tm order (scripts/gemm_res_ab.py,
 // profiles/r03/gemm_res_ab.log;
 // the N = 256 shapes and the plain e16 residual kind 3 measured equal or slower there and stay on the 8-phase
-// kernels); fast path bit 1024 turns it off (A/B)
+// kernels); and the fp32 row-remapped kind (12: the patch embedding's periodic positional addend onto the fp32
+// encoder stream, M = B*4096, N = K = 768), which the 8-phase kernels only run through the general register
+// epilogue; fast path bit 1024 turns both off (A/B)
 static int g_gemm4w_res = 1;
 static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off: A/B)
 template <int EPI>
@@ -1971,6 +1973,7 @@ int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
     case 4: return launch_gemm4w_fe<EPI, 4>(k, a, s);
     case 8: return launch_gemm4w_fe<EPI, 8>(k, a, s);
     case 11: return launch_gemm4w_fe<EPI, 11>(k, a, s);
+    case 12: return launch_gemm4w_fe<EPI, 12>(k, a, s);
     default: return -1;
   }
 }
@@ -2469,7 +2472,8 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
           a->batch == 1 && am == 0 && bm == 0 &&
           a->M >= 4096 &&
           (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8 ||
-           (g_gemm4w_res && k.fast_epi == 11 && a->K <= 512 && a->N % 256 != 0)) &&
+           (g_gemm4w_res && k.fast_epi == 11 && a->K <= 512 && a->N % 256 != 0) ||
+           (g_gemm4w_res && k.fast_epi == 12)) &&
           (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 40)) {
         t_last_path = 2;
         if (a->act == OCTSAM_ACT_GELU) return launch_gemm4w<OCTSAM_ACT_GELU>(k, a, s);

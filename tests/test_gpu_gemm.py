@@ -628,3 +628,29 @@ def test_gemm4w_broadcast_residual(cuda, N):
     ref = A.float() @ W.float().t() + bias + R.float().repeat(P, 1)
     assert _rel(outs[0], ref) < 5e-3
     assert torch.equal(outs[0], outs[1])
+
+
+def test_gemm4w_patch_embed_kind(cuda):
+    """The patch embedding's GEMM (fp32 encoder stream out, bias, the positional table as a periodic fp32 addend:
+    lean kind 12) on the two-workgroup kernel against torch fp32 and bit-identical to the 8-phase kernel's general
+    register epilogue (fast path bit 1024); timed for the record."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    L, B, N, K = 4096, 8, 768, 768
+    M = L * B
+    g = torch.Generator().manual_seed(12)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    pos = torch.randn(L, N, generator=g).to(cuda)
+    outs = []
+    for fast in (1, 1 | 1024):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(M, N, device=cuda, dtype=torch.float32)
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, residual=pos, r_remap=(L, B))
+        assert lib.octsam_gemm_last_path() == 2
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    ref = A.float() @ W.float().t() + bias + pos.repeat(B, 1)
+    assert _rel(outs[0], ref) < 5e-3
+    assert torch.equal(outs[0], outs[1])
