@@ -1878,6 +1878,48 @@ __device__ __forceinline__ void stage(const Src& s, int k0, char* buf, int wave)
 __device__ __forceinline__ e16x8 frag(const char* img, int row, int kc) {
   return *(const e16x8*)(img + row * 64 + ((kc ^ swz(row)) << 4));
 }
+// conv3x3 (a_mode 3: NHWC 64x64 images of C channels, k = tap * C + c): the A rows of one 32-wide K-step all read
+// one tap, so each issue's 16 rows are 16 shifted pixels; out-of-image pixels read a zero row (LDS-DMA cannot
+// zero-fill). A is re-addressed per stage; B as in make_src.
+__device__ __attribute__((aligned(16))) e16 g_zero_row[4096] = {};
+struct ConvSrc {
+  const e16* img;  // batch image base
+  int y[4], x[4], c;  // the lane's A row per A issue, its 16-B chunk (swizzled) within the row
+};
+__device__ __forceinline__ ConvSrc make_conv_src(const GemmK& p, const e16* A, int row0, int wave, int lane) {
+  ConvSrc s;
+  const int rr = lane >> 2, slot = lane & 3;
+  s.img = A + (long long)(row0 >> 12) * 4096 * p.conv_c;  // a 256-row tile stays inside one image (M % 4096 == 0)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int g = row0 + (wave * 4 + u) * 16 + rr;
+    s.y[u] = (g >> 6) & 63;
+    s.x[u] = g & 63;
+  }
+  s.c = slot;
+  return s;
+}
+__device__ __forceinline__ void stage_conv(const GemmK& p, const ConvSrc& cs, const Src& s, int k0, char* buf,
+                                           int wave, int lane) {
+  const int C = p.conv_c, tap = k0 / C, ch = k0 - tap * C, dy = tap / 3 - 1, dx = tap % 3 - 1;
+  const int rr = lane >> 2;
+#pragma unroll
+  for (int u = 0; u < OPS; ++u) {
+    const bool isA = u < 4;
+    const int j = isA ? wave * 4 + u : wave * 2 + (u - 4);
+    const e16* src;
+    if (isA) {
+      const int r = j * 16 + rr;
+      const int yy = cs.y[u] + dy, xx = cs.x[u] + dx;
+      const int c = cs.c ^ swz(r);
+      src = (yy >= 0 && yy < 64 && xx >= 0 && xx < 64) ? cs.img + ((long long)yy * 64 + xx) * C + ch + c * 8
+                                                       : g_zero_row + c * 8;
+    } else {
+      src = s.p[u] + k0;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(buf + (isA ? 0 : A_BYTES) + j * 1024), 16, 0, 0);
+  }
+}
 }  // namespace g4
 
 // one K-step of the wave's 128 x 64 tile: 8 A + 4 B fragment reads, 32 operand-swapped 16x16x32 MFMAs
@@ -1893,7 +1935,7 @@ __device__ __forceinline__ e16x8 frag(const char* img, int row, int kc) {
     __builtin_amdgcn_s_setprio(0);                                                                         \
   }
 
-template <int EPI, int FE>
+template <int EPI, int FE, bool CONV = false>
 __global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1911,18 +1953,24 @@ __global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
   const e16* B = (const e16*)p.B + bz * p.sB;
   const int nk = p.K / g4::KS;
   const g4::Src src = g4::make_src(p, A, B, row0, col0, wave, lane);
+  g4::ConvSrc csrc{};
+  if constexpr (CONV) csrc = g4::make_conv_src(p, A, row0, wave, lane);
+  auto stage = [&](int k0, char* buf) {
+    if constexpr (CONV) g4::stage_conv(p, csrc, src, k0, buf, wave, lane);
+    else g4::stage(src, k0, buf, wave);
+  };
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
   f32x4 acc[8][4];
 
-  g4::stage(src, 0, gsm, wave);
-  if (nk > 1) g4::stage(src, g4::KS, gsm + g4::STAGE, wave);
+  stage(0, gsm);
+  if (nk > 1) stage(g4::KS, gsm + g4::STAGE);
   // K-step t: stage t resident (stage t + 1 may stay in flight), every wave past step t - 1's fragment reads ->
   // stage t + 2 refills the buffer of step t - 1
   for (int t = 0; t < nk; ++t) {
     if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
-    if (t + 2 < nk) g4::stage(src, (t + 2) * g4::KS, gsm + ((t + 2) % g4::NS) * g4::STAGE, wave);
+    if (t + 2 < nk) stage((t + 2) * g4::KS, gsm + ((t + 2) % g4::NS) * g4::STAGE);
     const char* ca = gsm + (t % g4::NS) * g4::STAGE;
     const char* cb = ca + g4::A_BYTES;
     if (t == 0) G4_STEP(ca, cb, true) else G4_STEP(ca, cb, false)
@@ -1935,18 +1983,19 @@ __global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
   }
 }
 
-template <int EPI, int FE>
+template <int EPI, int FE, bool CONV = false>
 int launch_gemm4w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + 127) / 128;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<EPI, FE, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              g4::LDS);
     attr = true;
   }
   const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
-  hipLaunchKernelGGL((gemm4w_kernel<EPI, FE>), dim3((unsigned)nwg), dim3(256), g4::LDS, s, g);
+  hipLaunchKernelGGL((gemm4w_kernel<EPI, FE, CONV>), dim3((unsigned)nwg), dim3(256), g4::LDS, s, g);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
 }
@@ -2514,6 +2563,14 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   if (am == 1 && bm == 0) return launch<1, 0>(k, a->batch, s);
   if (am == 1 && bm == 1) return launch<1, 1>(k, a->batch, s);
   if (am == 2 && bm == 0) return launch<2, 0>(k, a->batch, s);
+  // conv3x3 on the two-workgroup kernel (the neck: M = B*4096, N = C = 256, K = 9C; fp32 C, no activation)
+  if (am == 3 && bm == 0 && g_gemm4w_res && g_use_glds == 1 && a->conv_c % 32 == 0 && a->conv_c <= 4096 &&
+      a->batch == 1 && a->act == 0 && (k.fast_epi == 1 || k.fast_epi == 2) && ((uintptr_t)a->A & 15) == 0 &&
+      (a->ldb & 7) == 0 && ((uintptr_t)a->B & 15) == 0) {
+    t_last_path = 2;
+    if (k.fast_epi == 1) return launch_gemm4w_fe<0, 1, true>(k, a, s);
+    return launch_gemm4w_fe<0, 2, true>(k, a, s);
+  }
   if (am == 3 && bm == 0) return launch<3, 0>(k, a->batch, s);
   if (am == 4 && bm == 0) return launch<4, 0>(k, a->batch, s);
   if (am == 1 && bm == 2) return launch<1, 5>(k, a->batch, s);

@@ -654,3 +654,27 @@ def test_gemm4w_patch_embed_kind(cuda):
     ref = A.float() @ W.float().t() + bias + pos.repeat(B, 1)
     assert _rel(outs[0], ref) < 5e-3
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("C", [256, 64])
+def test_gemm4w_conv3x3(cuda, C):
+    """The neck's conv3x3 (implicit GEMM over NHWC 64x64 images, zero padding through the zero row) on the
+    two-workgroup kernel against torch fp32 conv2d and the generic register-staged path (fast path bit 1024)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(C)
+    B, Co = 2, 256
+    x = torch.randn(B, 64, 64, C, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(Co, C, 3, 3, generator=g) / (3 * C ** 0.5)).to(cuda, torch.bfloat16)
+    Wr = W.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous()
+    outs = []
+    for fast in (1, 1 | 1024):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(B * 4096, Co, device=cuda)
+        kernels.gemm(x, Wr, M=B * 4096, N=Co, K=9 * C, out=out, a_mode=3, conv_c=C)
+        outs.append((out, lib.octsam_gemm_last_path()))
+    lib.octsam_gemm_set_fast_path(1)
+    assert outs[0][1] == 2 and outs[1][1] == 0
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), W.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    for out, _ in outs:
+        assert _rel(out, ref) < 1e-5
