@@ -12,8 +12,9 @@
 //   * the column scan of each augmenting step runs on the 64 lanes of one wave (one workgroup per map) and
 //     its argmin takes the lowest column index among equal minima — the host loop's first strict minimum;
 //   * the transport cost is summed in the host's order by one lane; per entry the costs are summed in map
-//     order, rounded to float, and the gradient is scattered into the map's row in the host's order
-//     (creators, then destroyers) in LDS by one lane, the row written out by the workgroup;
+//     order, rounded to float, and the gradient is scattered into the map's row in LDS with the host's
+//     per-pixel addition order (creators, then destroyers): one thread per contribution, a pixel hit several
+//     times summed in that order by the thread of its first contribution; the row written out by the workgroup;
 //   * no FMA contraction anywhere (the host build has none).
 // Bit-identity holds for q = 2 (the call site's loss_q: **2 is one fp32 multiply, the 1/q power a
 // correctly rounded sqrt on both sides); other q use pow on both sides (device ocml vs host libm may
@@ -266,38 +267,60 @@ __global__ void __launch_bounds__(256) w2_loss_kernel(const int32_t* __restrict_
     return;
   }
   if (!want_grad) return;
+  float* out = dpred + (size_t)k * nvals;
+  if (status[0]) {  // a pair-buffer overflow anywhere: the step's topological gradient is NaN, like its loss
+    for (int i = t; i < nvals; i += 256) out[i] = __builtin_nanf("");
+    return;
+  }
   float* row = (float*)w2_smem;
-  for (int i = t; i < nvals; i += 256) row[i] = 0.0f;
-  __syncthreads();
-  const int e = map_entry[k];
-  if (t == 0 && e >= 0) {
-    const int n = min(cnt[k * 3 + feat_col], max_pairs);
-    const double dd = w2_droot(entry_tot(e), q);
-    const float scale = (float)(lamda / n_entries * dd);
-    const int32_t* p1 = pairs + (size_t)k * max_pairs * 2;
-    const int32_t* p2 = pairs + (size_t)(Kn + k) * max_pairs * 2;
-    const float* v1 = vals + (size_t)k * nvals;
-    const float* v2 = vals + (size_t)(Kn + k) * nvals;
-    const int32_t* mk = match + (size_t)k * max_pairs;
-    // the host's two passes over the points: creators, then destroyers
-    for (int pass = 0; pass < 2; ++pass) {
-      for (int i = 0; i < n; ++i) {
-        const int j = mk[i];
-        const float d1p[2] = {v1[p1[2 * i]], v1[p1[2 * i + 1]]};
-        float d2p[2] = {0.0f, 0.0f};
-        if (j >= 0) {
-          d2p[0] = v2[p2[2 * j]];
-          d2p[1] = v2[p2[2 * j + 1]];
-        }
-        float g0, g1;
-        w2_grad_point(d1p, d2p, 0, j >= 0 ? 0 : -1, q, &g0, &g1);
-        const int px = p1[2 * i + pass];
-        row[px] += scale * (pass == 0 ? g0 : g1);
-      }
-    }
+  int* hits = (int*)(row + nvals);  // contributions per pixel
+  for (int i = t; i < nvals; i += 256) {
+    row[i] = 0.0f;
+    hits[i] = 0;
   }
   __syncthreads();
-  float* out = dpred + (size_t)k * nvals;
+  const int e = map_entry[k];
+  const int n = e >= 0 ? min(cnt[k * 3 + feat_col], max_pairs) : 0;
+  const int32_t* p1 = pairs + (size_t)k * max_pairs * 2;
+  const int32_t* p2 = pairs + (size_t)(Kn + k) * max_pairs * 2;
+  const float* v1 = vals + (size_t)k * nvals;
+  const float* v2 = vals + (size_t)(Kn + k) * nvals;
+  const int32_t* mk = match + (size_t)k * max_pairs;
+  // The host adds the 2n contributions in the order o = pass * n + i (creators, then destroyers) into a zeroed
+  // row. Here thread o computes contribution o; a pixel hit once gets 0 + c, a pixel hit several times is summed
+  // by the thread of its first contribution, in o order — the same fp32 additions, so the row is bit-identical.
+  for (int o = t; o < 2 * n; o += 256) atomicAdd(&hits[p1[2 * (o % n) + o / n]], 1);
+  float scale = 0.0f;
+  if (n > 0) scale = (float)(lamda / n_entries * w2_droot(entry_tot(e), q));
+  __syncthreads();
+  auto contrib = [&](int o) -> float {
+    const int i = o % n, pass = o / n;
+    const int j = mk[i];
+    const float d1p[2] = {v1[p1[2 * i]], v1[p1[2 * i + 1]]};
+    float d2p[2] = {0.0f, 0.0f};
+    if (j >= 0) {
+      d2p[0] = v2[p2[2 * j]];
+      d2p[1] = v2[p2[2 * j + 1]];
+    }
+    float g0, g1;
+    w2_grad_point(d1p, d2p, 0, j >= 0 ? 0 : -1, q, &g0, &g1);
+    return scale * (pass == 0 ? g0 : g1);
+  };
+  for (int o = t; o < 2 * n; o += 256) {
+    const int px = p1[2 * (o % n) + o / n];
+    if (hits[px] == 1) {
+      row[px] = 0.0f + contrib(o);
+      continue;
+    }
+    bool first = true;
+    for (int x = 0; x < o && first; ++x) first = p1[2 * (x % n) + x / n] != px;
+    if (!first) continue;
+    float acc = 0.0f;
+    for (int x = o; x < 2 * n; ++x)
+      if (p1[2 * (x % n) + x / n] == px) acc += contrib(x);
+    row[px] = acc;
+  }
+  __syncthreads();
   for (int i = t; i < nvals; i += 256) out[i] = row[i];
 }
 
@@ -327,7 +350,8 @@ extern "C" int octsam_topo_w2(const int32_t* pairs, const int32_t* cnt, const fl
   OCTSAM_CHECK_ARG(workspace_bytes >= octsam_topo_w2_workspace(Kn, max_pairs),
                    "octsam_topo_w2: workspace of %lld bytes, need %lld", (long long)workspace_bytes,
                    (long long)octsam_topo_w2_workspace(Kn, max_pairs));
-  OCTSAM_CHECK_ARG((size_t)nvals * 4 <= 65536, "octsam_topo_w2: nvals %d above the 64 KB gradient row", nvals);
+  OCTSAM_CHECK_ARG((size_t)nvals * 8 <= 65536, "octsam_topo_w2: nvals %d above the 64 KB gradient row + hit counts",
+                   nvals);
   hipStream_t s = (hipStream_t)stream;
   const W2Layout L(max_pairs);
   int dev = 0, lds_max = 0;
@@ -351,7 +375,7 @@ extern "C" int octsam_topo_w2(const int32_t* pairs, const int32_t* cnt, const fl
   w2_map_kernel<<<Kn, W2_THREADS, lds ? L.bytes : 0, s>>>(pairs, cnt, vals, Kn, max_pairs, nvals, feat_col, q, costs,
                                                            match, status, gscratch, lds ? 1 : 0);
   OCTSAM_LAUNCH_CHECK("octsam_topo_w2 (transport)");
-  w2_loss_kernel<<<Kn + 1, 256, want_grad ? (size_t)nvals * 4 : 0, s>>>(
+  w2_loss_kernel<<<Kn + 1, 256, want_grad ? (size_t)nvals * 8 : 0, s>>>(
       pairs, cnt, vals, Kn, max_pairs, nvals, feat_col, q, lamda, entry_maps, entry_off, map_entry, n_entries, costs,
       match, status, want_grad, loss_out, dpred);
   OCTSAM_LAUNCH_CHECK("octsam_topo_w2 (loss)");

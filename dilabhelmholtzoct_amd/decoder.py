@@ -328,7 +328,7 @@ class MaskDecoder(nn.Module):
             return out
         beta = 1.0 if accumulate else 0.0
         if (split is None and self.wide_wgrad and M >= 65536 and K.wgrad_supported(M, O, I) and ldy % 8 == 0
-                and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0):
+                and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and out.is_contiguous()):
             # image side: one workgroup per CU holds the whole O x I output and streams its rows (octsam_wgrad)
             K.wgrad(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db, dbx=dbx, dbx_fold=dbx_fold)
             return out

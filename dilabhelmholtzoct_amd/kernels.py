@@ -106,6 +106,8 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, M: int, out: torch.Tensor, *, ldy: 
     ldx = I if ldx is None else ldx
     if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32:
         raise ValueError("wgrad: bf16 operands and an fp32 output")
+    if not out.is_contiguous():
+        raise ValueError("wgrad: out must be contiguous (the final reduction writes O*I floats from its base)")
     for name, t in (("db", db), ("dbx", dbx)):
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
             raise ValueError(f"wgrad: {name} must be contiguous fp32")

@@ -31,16 +31,17 @@ class _Phases:
 
 
 class FusedTrainStep:
-    """One training step of the reference (training_utils.py:46-69) as three phases:
+    """One training step of the reference (training_utils.py:46-69) as four phases:
 
       E  image encoder forward                        (reads no trainable weight)
-      F  prompt tokens, decoder forward, post-processing, DiceCE fwd/bwd, topo-loss device forward (PH), D2H of the
-         persistence pairs
-      -- host: W2 between diagrams (POT emd2 restated) -> d topo / d map, topo loss
-      B  H2D of the topo gradient, topo backward, post-processing backward, decoder backward
-      then (world > 1) the RCCL all-reduce of the flat decoder gradient and Adam.
+      F  prompt tokens, decoder forward, post-processing, DiceCE forward, topo resampling + persistence (PH) and,
+         with w2="device" (default), the W2 transport, topo loss and d topo / d map on the GPU (octsam_topo_w2)
+      F2 DiceCE backward (the W2 of w2="device" forks beside it when fork_topo)
+      B  topo backward, post-processing backward, decoder backward, loss assembly
+      then (world > 1) the RCCL all-reduce of the flat decoder gradient and Adam. No host work or device sync sits
+      inside a step; w2="host" keeps the round-2 path (pairs D2H after F, octsam_topo_host on the host, H2D before B).
 
-    graphs=True captures E, F and B as hipGraphs (one pool, replayed in capture order) the first time a
+    graphs=True captures E, F, F2 and B as hipGraphs (one pool, replayed in capture order) the first time a
     batch shape is seen, after eager warm-up, and replays them afterwards: no per-kernel host launch cost.
     In data-parallel runs (overlap=True) the all-reduce runs on a side stream and Adam is deferred to the
     next step, after that step's encoder forward has been queued: the gradient exchange overlaps the
@@ -74,7 +75,9 @@ class FusedTrainStep:
         self._pe = None
         self.graphs = graphs
         self.overlap = overlap and process_group is not None
-        self._graphs = {}       # batch shape -> captured graphs + static input copies (graph mode)
+        self._graphs = {}       # batch shape -> captured graphs + static input copies (graph mode), LRU order
+        self.captures = 0       # graph sets captured (recaptures after an eviction included)
+        self.evictions = 0
         self._pending = None    # (event, ) of an all-reduce whose Adam step has not run yet
         self._side = None
         self.pipeline = pipeline and graphs
@@ -250,9 +253,12 @@ class FusedTrainStep:
     def _graph_key(self, *ts):
         return tuple((None if t is None else (tuple(t.shape), t.dtype)) for t in ts)
 
-    # captured step graphs kept (one per batch shape: B, the prompt count N, prompt kind; x2 encoder-lookahead
-    # parities): an epoch of the training loop sees a handful of prompt counts
-    MAX_GRAPHS = 16
+    # captured step graphs kept, least recently used evicted (one set per batch shape: B, the prompt count N, prompt
+    # kind; x2 encoder-lookahead parities). N is the batch's largest component count and cannot be bucketed: the
+    # collate's zero-padded prompts enter the reference's DiceCE mean, so padding N further would change the loss.
+    # A set's private pool holds the step's activations, ~1.5-2 GB at B = 8, N ~ 21 (vit-b), so 32 sets stay far
+    # below 288 GB; `captures` / `evictions` count recaptures (a capture = one eager pass + 3 captures + a sync).
+    MAX_GRAPHS = 32
 
     def _encoder_set(self, ekey, pixel_values):
         """Captured encoder graph E for one pixel shape and parity: its own memory pool, a static pixel input and
@@ -326,8 +332,10 @@ class FusedTrainStep:
         static = (None, gt_u8, input_boxes, input_points, input_labels)  # pixels: the encoder set's input
         g = {"graphs": (gf, gf2, gb), "eset": es, "st": st, "ev": torch.cuda.Event(), "static": static}
         self._graphs[key] = g
+        self.captures += 1
         while len(self._graphs) > self.MAX_GRAPHS:
             self._graphs.pop(next(iter(self._graphs)))
+            self.evictions += 1
         return g
 
     @staticmethod
@@ -363,9 +371,11 @@ class FusedTrainStep:
         ekey0 = (tuple(pixel_values.shape), pixel_values.dtype)
         par = self._parity.get(ekey0, 0) if self.pipeline else 0
         ekey = ekey0 + (par,)
-        g = self._graphs.get(key + (par,))
+        g = self._graphs.pop(key + (par,), None)
         if g is None:
             g = self._capture(key + (par,), inputs, crop, orig, global_batch, ekey)
+        else:
+            self._graphs[key + (par,)] = g  # most recently used last
         es = g["eset"]
         gf, gf2, gb = g["graphs"]
         st, ev = g["st"], g["ev"]
@@ -444,6 +454,33 @@ class FusedTrainStep:
         bc2 = 1.0 - b2 ** self.t
         K.adam(dec.flat, dec.flat_grad, self.exp_avg, self.exp_avg_sq, beta1=b1, beta2=b2, eps=self.eps,
                weight_decay=self.wd, step_size=self.lr / bc1, bc2_sqrt=math.sqrt(bc2), params_bf16=dec.flat_b16)
+
+    @torch.no_grad()
+    def optimizer_state(self) -> dict:
+        """Adam state with HF names: "exp_avg.mask_decoder.<param>" / "exp_avg_sq.mask_decoder.<param>" (fp32, CPU,
+        the parameters' HF shapes) and "step" (torch.optim.Adam's per-parameter step count; one shared count here)."""
+        self.flush()
+        dec = self.model.mask_decoder
+        out = {"step": torch.tensor(float(self.t))}
+        for name in dec._order:
+            for key, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+                out[f"{key}.mask_decoder.{name}"] = dec._param_view(buf, name).detach().float().cpu().contiguous()
+        return out
+
+    @torch.no_grad()
+    def load_optimizer_state(self, state: dict):
+        """Resume Adam from optimizer_state()'s layout (e.g. a torch.optim.Adam run converted by name), so a
+        continued run takes the same update as the optimizer it replaces instead of a cold first step."""
+        self.flush()
+        dec = self.model.mask_decoder
+        for name in dec._order:
+            for key, buf in (("exp_avg", self.exp_avg), ("exp_avg_sq", self.exp_avg_sq)):
+                src = state[f"{key}.mask_decoder.{name}"]
+                view = dec._param_view(buf, name)
+                if tuple(src.shape) != tuple(view.shape):
+                    raise ValueError(f"{key} of {name}: shape {tuple(src.shape)} != {tuple(view.shape)}")
+                view.copy_(src.to(device=buf.device, dtype=torch.float32))
+        self.t = int(float(state["step"]))
 
     def _launch_update(self, n_local, n_global):
         """All-reduce (side stream when overlapping) then Adam, now or at the next _finish_pending."""
@@ -756,6 +793,7 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
         step.flush()
         epoch_loss = float(_collective_sum(loss_acc, pg)[0]) / len(batches)
         hist["train_time_s"].append(time.perf_counter() - t_epoch)
+        hist.setdefault("graph_captures", []).append(step.captures)  # cumulative; > 2 per shape = recaptures
         vloss = validate_model(step, vds, processor, bs, config, world, rank, pg, device, device_data)
         hist["train_loss"].append(epoch_loss)
         hist["valid_loss"].append(vloss)

@@ -1,7 +1,10 @@
-"""One training step of BASELINE configs[3] / configs[4]'s per-GPU slices on the HIP path against the oracle
+"""One training step of BASELINE configs[1] - configs[4]'s per-GPU slices on the HIP path against the oracle
 (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE / topo loss, run on the GPU here only for
 speed) on the same synthetic weights and batch:
 
+* configs[1]: sam-vit-base, box prompts, --top=False, bf16, 8 images per GPU (the DiceCE-only step,
+  ref:octsam/models/training_utils.py:62-68 with topological=False);
+* configs[2]: the same with --top=True (the bench's workload);
 * configs[3]: sam-vit-large, point prompts, --top=True, bf16, 4 images per GPU (batch 32 over 8 GPUs);
 * configs[4]: sam-vit-huge, a box and a point per component, --top=True, 8 images per GPU (batch 64 over 8
   GPUs), with the bf16 encoder and with the fp16 encoder (the configuration's precision).
@@ -15,10 +18,12 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-CASES = {
-    "vitl_points_b4_bf16": ("facebook/sam-vit-large", "points", 4, torch.bfloat16),
-    "vith_both_b8_bf16": ("facebook/sam-vit-huge", "both", 8, torch.bfloat16),
-    "vith_both_b8_fp16": ("facebook/sam-vit-huge", "both", 8, torch.float16),
+CASES = {  # name: (model, prompt, images, encoder dtype, topological)
+    "vitb_bboxes_b8_top_off": ("facebook/sam-vit-base", "bboxes", 8, torch.bfloat16, False),
+    "vitb_bboxes_b8_top_on": ("facebook/sam-vit-base", "bboxes", 8, torch.bfloat16, True),
+    "vitl_points_b4_bf16": ("facebook/sam-vit-large", "points", 4, torch.bfloat16, True),
+    "vith_both_b8_bf16": ("facebook/sam-vit-huge", "both", 8, torch.bfloat16, True),
+    "vith_both_b8_fp16": ("facebook/sam-vit-huge", "both", 8, torch.float16, True),
 }
 
 
@@ -33,7 +38,7 @@ def test_step_vs_oracle(cuda, case):
     from dilabhelmholtzoct_amd.model import SamModel
     from dilabhelmholtzoct_amd.train import FusedTrainStep
     from oracle.step_ref import CpuReferenceStep, synthetic_state_dict
-    name, prompt, B, edt = CASES[case]
+    name, prompt, B, edt, top = CASES[case]
     state = synthetic_state_dict(name, seed=0)
     sd = data.SAMDataset(data.synthetic_oct(seed=31, n=B), {"prompt_type": prompt}, epoch_seed=0)
     b = data.process_batch(data.make_processor(), data.custom_collate([sd[i] for i in range(B)]), prompt)
@@ -44,7 +49,7 @@ def test_step_vs_oracle(cuda, case):
     ours = ours.to(cuda)
     if edt == torch.float16:
         ours.set_encoder_dtype(torch.float16)
-    step = FusedTrainStep(ours, topological=True)
+    step = FusedTrainStep(ours, topological=top)
     crop = tuple(int(v) for v in b["reshaped_input_sizes"][0])
     orig = tuple(int(v) for v in b["original_sizes"][0])
     loss = step.forward_backward(bd["pixel_values"], bd["gt_u8"], input_boxes=bd.get("input_boxes"),
@@ -55,7 +60,7 @@ def test_step_vs_oracle(cuda, case):
     del ours, step
     torch.cuda.empty_cache()
 
-    ref = CpuReferenceStep(name, topological=True, state_dict=state, device=cuda, loss_device=cuda)
+    ref = CpuReferenceStep(name, topological=top, state_dict=state, device=cuda, loss_device=cuda)
     ref.opt.zero_grad()
     rl, rtopo, _ = ref.forward_loss(b)
     rl.backward()
@@ -64,6 +69,8 @@ def test_step_vs_oracle(cuda, case):
     print(f"{case}: DiceCE {dicece:.6f} (oracle {rdicece:.6f}), topo {float(loss[2]):.6f} (oracle {rtopo:.6f})")
     assert abs(dicece - rdicece) <= 1e-3 * abs(rdicece), (dicece, rdicece)
     assert abs(float(loss[2]) - rtopo) <= 2e-2 * abs(rtopo) + 1e-6, (float(loss[2]), rtopo)
+    if not top:
+        assert float(loss[2]) == 0.0 and rtopo == 0.0, (float(loss[2]), rtopo)
 
     rg = {n: p.grad.double().cpu() for n, p in ref.model.mask_decoder.named_parameters() if p.grad is not None}
     scale = max(g.norm().item() for g in rg.values())

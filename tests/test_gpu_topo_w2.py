@@ -6,7 +6,7 @@ replaces in the training step): bit-identical loss and d loss / d pred values on
   paths), and the pair-buffer sizes of 50x50 maps (LDS scratch) and 64x63 maps (global-memory scratch);
 * real persistence diagrams: 50x50 sigmoid maps of random logits and gt-like binary maps through the HIP
   persistence kernel, "first" and "all" modes;
-* an overflowing pair count -> NaN loss (the host raises).
+* an overflowing pair count -> NaN loss and NaN gradient rows (the host raises).
 """
 import math
 
@@ -91,8 +91,9 @@ def test_device_w2_overflow_gives_nan(cuda):
     from dilabhelmholtzoct_amd.losses import topo_w2_device
     pairs, cnt, vals = _case(4, 1, [2, 2])
     cnt[0, 2] = 1
-    loss, _ = topo_w2_device(*(torch.from_numpy(a).to(cuda) for a in (pairs, cnt, vals)), [[0]], [0])
+    loss, grad = topo_w2_device(*(torch.from_numpy(a).to(cuda) for a in (pairs, cnt, vals)), [[0]], [0])
     assert math.isnan(float(loss.cpu()[0]))
+    assert bool(torch.isnan(grad).all()), "an overflowed step must not hand Adam a finite topo gradient"
 
 
 @pytest.mark.parametrize("mode", ["first", "all"])
