@@ -39,19 +39,24 @@ def batches(seed, n, bs, epoch):
 
 
 def oracle_adam_state(ref) -> dict:
+    """torch Adam state by HF name; parameters that never received a gradient (the IoU head: the loss does not use
+    it) have no state in torch and zero moments in the fused Adam, so they are exported as zeros."""
     out = {}
     step = None
     for name, p in ref.model.mask_decoder.named_parameters():
-        st = ref.opt.state[p]
-        step = float(st["step"])
-        out[f"exp_avg.mask_decoder.{name}"] = st["exp_avg"].detach().cpu()
-        out[f"exp_avg_sq.mask_decoder.{name}"] = st["exp_avg_sq"].detach().cpu()
+        st = ref.opt.state.get(p, {})
+        if "step" in st:
+            step = float(st["step"])
+        out[f"exp_avg.mask_decoder.{name}"] = st["exp_avg"].detach().cpu() if st else torch.zeros_like(p).cpu()
+        out[f"exp_avg_sq.mask_decoder.{name}"] = st["exp_avg_sq"].detach().cpu() if st else torch.zeros_like(p).cpu()
     out["step"] = torch.tensor(step)
     return out
 
 
 def load_oracle_adam(ref, state):
     for name, p in ref.model.mask_decoder.named_parameters():
+        if not bool(state[f"exp_avg_sq.mask_decoder.{name}"].any()):
+            continue  # no state in torch for a parameter that never had a gradient
         ref.opt.state[p] = {"step": torch.tensor(float(state["step"])),
                             "exp_avg": state[f"exp_avg.mask_decoder.{name}"].to(p.device, torch.float32).clone(),
                             "exp_avg_sq": state[f"exp_avg_sq.mask_decoder.{name}"].to(p.device, torch.float32).clone()}
