@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--e2e-steps", type=int, default=10,
                    help="steps of the end-to-end loop (a new batch per step through the HIP data path)")
     p.add_argument("--topo-all", type=int, default=1, help="time the topo_mode='all' reading of batch_iter too")
+    p.add_argument("--top-off", type=int, default=1,
+                   help="with --top 1: also time the --top=False step on the same batch (BASELINE configs[1])")
     p.add_argument("--loop-images", type=int, default=128,
                    help="time train.training() over an epoch of this many synthetic images (0 = skip)")
     return p.parse_args()
@@ -390,6 +392,31 @@ def topo_all_sensitivity(args, model, batch, steps=5):
     return out
 
 
+def top_off_leg(args, model, batch, steps=10):
+    """BASELINE configs[1] beside the headline configs[2]: the same model, batch and execution (hipGraphs + encoder
+    lookahead) with --top=False (the DiceCE-only step, ref:octsam/models/training_utils.py:62-68), timed like the
+    headline (inputs resident, `steps` back-to-back steps, the last one naming no next batch)."""
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    pipe = bool(args.pipeline) and not args.eager
+    B = batch["gt_u8"].shape[0]
+    st = FusedTrainStep(model, lr=1e-3, topological=False, graphs=not args.eager, pipeline=pipe)
+    for i in range(3):
+        st.step(batch, next_batch=batch if i < 2 else None)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        st.step(batch, next_batch=batch if i + 1 < steps else None)
+    st.flush()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del st
+    out = {"workload": "configs[1]: sam-vit-base, --prompt=bboxes, --top=False, bf16, B=8 per GPU",
+           "value": round(B * steps / dt, 4), "unit": "imgs/s", "ms_per_step": round(dt * 1e3 / steps, 3),
+           "steps": steps}
+    log(f"top off (configs[1]): {out}")
+    return out
+
+
 def time_training_loop(args, device, n_images=128):
     """The drop-in loop itself (train.training, ref:octsam/models/training.py:184 -> training_utils.py:27-80) over a
     synthetic n_images-image epoch: its defaults (hipGraphs + encoder lookahead, HIP data path on a side stream),
@@ -651,6 +678,9 @@ def main():
     topo_all = None
     if args.topo_all and args.top and rank == 0 and world == 1:
         topo_all = topo_all_sensitivity(args, model, batch)
+    top_off = None
+    if args.top_off and args.top and rank == 0 and world == 1:
+        top_off = top_off_leg(args, model, batch, steps=args.steps)
     loop = None
     if args.loop_images and rank == 0 and world == 1 and not args.eager:
         loop = time_training_loop(args, device, args.loop_images)
@@ -703,6 +733,7 @@ def main():
             "end_to_end": e2e,
             "training_loop": loop,
             "topo_mode_all": topo_all,
+            "top_off": top_off,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -7,7 +7,9 @@ share a pass on gfx950; MI355X_MICROARCH.md §HBM, §rocprofv3 PMC slots):
 
 FETCH_SIZE / WRITE_SIZE are in KiB. gfx950 correction: FETCH_SIZE reports half the bytes of wide
 (16 B/lane) streaming reads, global_load_lds included -> doubled; WRITE_SIZE is exact for 16-B stores.
-Usage: pmc_traffic.py <dir> <kernel-name-substring> [out.json]"""
+Usage: pmc_traffic.py <dir> <kernel-name-substring[,substring...]> [out.json]
+A comma-separated list sums the dispatches of every listed kernel (bench.py's roofline family, octsam_gemm path 2:
+gemm8_kernel,gemm8p_kernel,gemm4w_kernel -- the same launch set as its compulsory_bytes_per_launch)."""
 import csv
 import glob
 import json
@@ -15,14 +17,14 @@ import os
 import sys
 
 
-def per_dispatch(d, counter, kname):
+def per_dispatch(d, counter, knames):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if counter not in r.get("Counter_Name", "") or kname not in r.get("Kernel_Name", ""):
+            if counter not in r.get("Counter_Name", "") or not any(k in r.get("Kernel_Name", "") for k in knames):
                 continue
             key = (r.get("Dispatch_Id"), r.get("Agent_Id"))
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
@@ -31,8 +33,9 @@ def per_dispatch(d, counter, kname):
 
 def main():
     d, kname = sys.argv[1], sys.argv[2]
-    fetch = per_dispatch(os.path.join(d, "fetch"), "FETCH_SIZE", kname)
-    write = per_dispatch(os.path.join(d, "write"), "WRITE_SIZE", kname)
+    knames = [k for k in kname.split(",") if k]
+    fetch = per_dispatch(os.path.join(d, "fetch"), "FETCH_SIZE", knames)
+    write = per_dispatch(os.path.join(d, "write"), "WRITE_SIZE", knames)
     res = {"kernel": kname, "dispatches": [len(fetch), len(write)],
            "fetch_bytes_per_launch": 2 * 1024 * sum(fetch) / max(len(fetch), 1),
            "write_bytes_per_launch": 1024 * sum(write) / max(len(write), 1)}

@@ -148,6 +148,9 @@ def main():
             fo.flush()
 
     start_w = {k: v.float() for k, v in load_file(START).items()}
+    warm_adam = None
+    if a.warm and a.mode == "spread":  # the spread along the warm-start trajectory (weights + Adam state)
+        start_w, warm_adam = split_warm(a.warm)
     if a.mode == "spread":
         val_cpu, val = R.val(3001)
         tr_by_ep = {ep: batches(2001, 128, a.bs, ep) for ep in range(a.epochs)}
@@ -163,9 +166,13 @@ def main():
                 model.load_state_dict(state)
                 model = model.to(dev)
                 st = FusedTrainStep(model, lr=a.lr, topological=True, graphs=True, pipeline=True)
+                if warm_adam is not None:
+                    st.load_optimizer_state(warm_adam)
                 conf = lambda: hip_conf(st, model, val)  # noqa: E731
             else:
                 ref = CpuReferenceStep(NAME, topological=True, lr=a.lr, state_dict=state, device=dev, loss_device=dev)
+                if warm_adam is not None:
+                    load_oracle_adam(ref, warm_adam)
                 conf = lambda: oracle_conf(ref, R, val_cpu, "v3001", bf)  # noqa: E731
             k = 0
             c = conf()

@@ -1,25 +1,33 @@
 """Val-Dice parity (BASELINE.json north_star: "val Dice within ±0.005 of the CPU reference on identical seeds") on
 SURVEY.md §8(d)'s protocol: 128 synthetic training scans and 32 held-out ones, B = 8, box prompts, --top=True,
-lr 1e-3 (the reference CLI's default), the reference's prompt redraw every epoch (SAMDataset.__getitem__).
+lr 1e-3 (the reference CLI's default), the reference's prompt redraw every epoch (SAMDataset.__getitem__), the
+held-out Dice after EVERY epoch asserted, not only the last.
 
 Start point. From the random initial weights every run first collapses to all-foreground masks (specificity ~0),
-and the step at which it leaves that state is chaotic — the same arithmetic in fp32 leaves it after ~112 steps on
-one data seed and not within 384 on another; the HIP path after ~112 / ~128 steps, torch's own bf16 autocast run
-after ~176 (profiles/r03/valdice_traj_*.jsonl). A Dice compared during or across that transition measures the
-chaos, not the implementation. Both sides therefore start from the decoder the fp32 oracle reached after 256 steps
-on another synthetic set (training seed 2000, held-out seed 3000: tests/golden/valdice_start_decoder.safetensors,
-made on MI355X by scripts/val_dice_traj.py --seed 0 --no-hip --save-at 256; encoder and prompt encoder: the
-synthetic weights, seed 0), which is past the transition.
+and the step at which it leaves that state is chaotic (profiles/r03/valdice_traj_*.jsonl). Both sides therefore
+start from a decoder past that transition: tests/golden/valdice_start_decoder.safetensors (the fp32 oracle after
+256 steps on another synthetic set, training seed 2000 / held-out seed 3000; encoder and prompt encoder: the
+synthetic weights, seed 0).
 
-Then both sides train the same EPOCHS epochs on this test's own 128 scans (seed 2001) and are scored on its 32
-held-out scans (seed 3001):
+Warm optimizer. Round 3 started both sides with a COLD Adam at that decoder: the first bias-corrected steps are
+lr-sized in every coordinate, both sides fall from Dice 0.79 to ~0.45 within 4 steps and climb back, and inside
+that dip the oracle's OWN spread under bf16-rounding-sized weight perturbations (1 + 2^-8 u per weight) or
+bf16-rounded image embeddings is 0.477-0.507 at step 16 (profiles/r04/valdice_spread.jsonl) -- a HIP-vs-oracle
+difference there (round 3: +0.025) measures that chaos, not the implementation. Here the start decoder first takes
+WARM steps of the same training on its own set (seed 2000; HIP, the start state only has to be identical on both
+sides), and BOTH sides then resume from those weights and that Adam state (FusedTrainStep.optimizer_state ->
+torch.optim.Adam state by name), so no cold first step sits inside the compared trajectory.
+
+Then both sides train EPOCHS epochs on this test's own 128 scans (seed 2001) and are scored on its 32 held-out
+scans (seed 3001) after every epoch:
 * ours: FusedTrainStep exactly as bench.py runs it (hipGraphs + the encoder lookahead), predict_masks +
   class_confusion (HIP confusion counts);
-* oracle: oracle/step_ref.py (transformers SamModel fp32 — on the GPU only to keep the test short; the frozen
-  encoder's embeddings computed once per batch — restated DiceCE / topo loss, torch Adam), scored by
+* oracle: oracle/step_ref.py (transformers SamModel fp32 -- on the GPU only to keep the test short; the frozen
+  encoder's embeddings computed once per batch -- restated DiceCE / topo loss, torch Adam), scored by
   oracle/eval_ref.pooled_confusion_ref (the reference's threshold and break quirk, training_utils.py:126-156).
-Asserted: the oracle is in the non-degenerate regime (mean specificity > 0.5 and Dice >= 0.1 above the
-random-init weights'), and |Dice_ours - Dice_oracle| <= 0.005 at the final checkpoint (no relaxed bound)."""
+Asserted: the oracle is in the non-degenerate regime (mean specificity > 0.5), the compared epochs actually trained
+(the oracle's decoder moved by more than 1 % in norm and its Dice changed), and |Dice_ours - Dice_oracle| <= 0.005
+at every epoch checkpoint."""
 import os
 
 import pytest
@@ -30,7 +38,8 @@ pytestmark = pytest.mark.gpu
 NAME = "facebook/sam-vit-base"
 TOL = 0.005
 LR = 1e-3
-EPOCHS = 2
+WARM = 64
+EPOCHS = 4
 BS = 8
 START = os.path.join(os.path.dirname(__file__), "golden", "valdice_start_decoder.safetensors")
 
@@ -44,6 +53,43 @@ def _epoch_batches(seed, n, epoch):
             for s in range(0, n, BS)]
 
 
+def warm_start(cuda, state):
+    """The start decoder after WARM steps on its own training set (seed 2000) with the HIP step: decoder weights
+    (fp32, HF names) and the Adam state (HF names)."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    model = SamModel(NAME)
+    model.load_state_dict(state)
+    model = model.to(cuda)
+    step = FusedTrainStep(model, lr=LR, topological=True, graphs=True, pipeline=True)
+    k, ep = 0, 0
+    while k < WARM:
+        tr = [data.to_device_batch(b, cuda) for b in _epoch_batches(2000, 128, ep)]
+        for i, b in enumerate(tr):
+            if k >= WARM:
+                break
+            step.step(b, next_batch=tr[i + 1] if i + 1 < len(tr) and k + 1 < WARM else None)
+            k += 1
+        ep += 1
+    adam = step.optimizer_state()
+    weights = {"mask_decoder." + n: t.detach().float().cpu().clone() for n, t in model.mask_decoder.state_dict().items()}
+    del step, model
+    torch.cuda.empty_cache()
+    return weights, adam
+
+
+def load_torch_adam(opt, module, adam):
+    """FusedTrainStep.optimizer_state() -> torch.optim.Adam state (parameters that never had a gradient, the IoU
+    head, keep no state in torch)."""
+    for name, p in module.named_parameters():
+        m, v = adam[f"exp_avg.mask_decoder.{name}"], adam[f"exp_avg_sq.mask_decoder.{name}"]
+        if not bool(v.any()):
+            continue
+        opt.state[p] = {"step": torch.tensor(float(adam["step"])), "exp_avg": m.to(p.device).clone(),
+                        "exp_avg_sq": v.to(p.device).clone()}
+
+
 def test_val_dice_parity(cuda):
     from safetensors.torch import load_file
     from dilabhelmholtzoct_amd import data
@@ -53,10 +99,19 @@ def test_val_dice_parity(cuda):
     from oracle.step_ref import CpuReferenceStep, synthetic_state_dict
 
     state = synthetic_state_dict(NAME, seed=0)
+    start = {k: v.float() for k, v in load_file(START).items()}
+    for k, v in start.items():
+        assert k in state and state[k].shape == v.shape, k
+        state[k] = v
+    weights, adam = warm_start(cuda, state)
+    state.update(weights)
+
     val_cpu = _epoch_batches(3001, 32, 0)
     val = [data.to_device_batch(v, cuda) for v in val_cpu]
     ref = CpuReferenceStep(NAME, topological=True, lr=LR, state_dict=state, device=cuda, loss_device=cuda)
+    load_torch_adam(ref.opt, ref.model.mask_decoder, adam)
     val_emb = [ref.embed(v) for v in val_cpu]
+    w0 = torch.cat([p.detach().flatten() for p in ref.model.mask_decoder.parameters()]).clone()
 
     def ref_conf():
         c = torch.zeros(14, 4, dtype=torch.int64)
@@ -65,17 +120,11 @@ def test_val_dice_parity(cuda):
                 c += pooled_confusion_ref(ref.predict(v, e), v["gt_u8"], v["mask_values"])
         return c
 
-    dice_init = mean_dice_ref(ref_conf())  # the random-init decoder
-    start = {k: v.float() for k, v in load_file(START).items()}
-    for k, v in start.items():
-        assert k in state and state[k].shape == v.shape, k
-        state[k] = v
-    ref.model.load_state_dict(state)
-    ref.opt = torch.optim.Adam(ref.model.mask_decoder.parameters(), lr=LR)
     ours = SamModel(NAME)
     ours.load_state_dict(state)
     ours = ours.to(cuda)
     step = FusedTrainStep(ours, lr=LR, topological=True, graphs=True, pipeline=True)
+    step.load_optimizer_state(adam)
 
     def ours_conf():
         step.flush()
@@ -90,6 +139,7 @@ def test_val_dice_parity(cuda):
     results = [(0, dice3(ours_conf()), mean_dice_ref(ref_conf()))]
     emb_cache = {}
     k = 0
+    c_ref = None
     for ep in range(EPOCHS):
         tr_cpu = _epoch_batches(2001, 128, ep)
         tr = [data.to_device_batch(b, cuda) for b in tr_cpu]
@@ -102,10 +152,13 @@ def test_val_dice_parity(cuda):
         c_ref = ref_conf()
         results.append((k, dice3(ours_conf()), mean_dice_ref(c_ref)))
     spec = mean_specificity_ref(c_ref)
+    w1 = torch.cat([p.detach().flatten() for p in ref.model.mask_decoder.parameters()])
+    moved = float((w1 - w0).norm() / w0.norm())
     for kk, got, want in results:
         print(f"after {kk:3d} steps: val Dice HIP {got:.5f}  oracle {want:.5f}  diff {got - want:+.5f}")
-    print(f"random-init Dice {dice_init:.5f}; oracle specificity at the end {spec:.4f}")
-    kk, got, want = results[-1]
+    print(f"oracle specificity at the end {spec:.4f}; oracle decoder moved {moved:.4f} (relative norm)")
     assert spec > 0.5, f"oracle specificity {spec:.4f}: the degenerate all-foreground regime"
-    assert want - dice_init >= 0.1, (want, dice_init)
-    assert abs(got - want) <= TOL, (kk, got, want)
+    assert moved > 0.01, f"the oracle's decoder barely moved ({moved:.4g}): the compared epochs did not train"
+    assert abs(results[-1][2] - results[0][2]) > 1e-4, "the oracle's val Dice never changed"
+    bad = [(kk, got, want) for kk, got, want in results if abs(got - want) > TOL]
+    assert not bad, f"|Dice_HIP - Dice_oracle| > {TOL} at {bad}"
