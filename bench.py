@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--e2e-steps", type=int, default=10,
                    help="steps of the end-to-end loop (a new batch per step through the HIP data path)")
     p.add_argument("--topo-all", type=int, default=1, help="time the topo_mode='all' reading of batch_iter too")
+    p.add_argument("--val-protocol", type=int, default=1,
+                   help="the val-Dice protocol of tests/test_gpu_val_dice.py beside the committed oracle values")
     p.add_argument("--top-off", type=int, default=1,
                    help="with --top 1: also time the --top=False step on the same batch (BASELINE configs[1])")
     p.add_argument("--loop-images", type=int, default=128,
@@ -417,6 +419,89 @@ def top_off_leg(args, model, batch, steps=10):
     return out
 
 
+def val_protocol(args, device):
+    """The val-Dice half of the metric on SURVEY.md §8(d)'s protocol, HIP side of tests/test_gpu_val_dice.py
+    (ref:octsam/models/training_utils.py:113-156, 246): the synthetic vit-b weights (seed 0) with the committed start
+    decoder, 64 warm steps on its own synthetic set, then 4 epochs (64 steps) on the test's 128 scans, the held-out
+    32 scans scored after every epoch, beside the fp32 oracle's values from the same protocol
+    (tests/golden/valdice_oracle.json, made by the test on MI355X). Batches come from the HIP data path (bit-identical
+    to the host SAMDataset + collate + SamProcessor path the test uses: test_gpu_training_loop.py); the step is the
+    benchmarked one (hipGraphs + encoder lookahead)."""
+    from safetensors.torch import load_file
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.components import collate_device
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
+    from dilabhelmholtzoct_amd.train import FusedTrainStep, class_confusion, mean_dice, predict_masks
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "valdice_oracle.json")))
+    name, bs, lr = "facebook/sam-vit-base", 8, 1e-3
+    t0 = time.perf_counter()
+    dproc = DeviceProcessor(device)
+    raw = {}
+
+    def epoch_batches(seed, n, epoch):
+        if seed not in raw:
+            ds = data.synthetic_oct(seed=seed, n=n)
+            raw[seed] = (np.stack([np.array(d["image"]) for d in ds]), np.stack([np.array(d["label"]) for d in ds]))
+        imgs, labs = raw[seed]
+        out = []
+        for s in range(0, n, bs):
+            e = min(n, s + bs)
+            hooks = [(lambda i=i: data.seed_sample(epoch, i, seed)) for i in range(s, e)]
+            b = collate_device(imgs[s:e], labs[s:e], "bboxes", device, seed_hooks=hooks, processor=dproc)
+            b.pop("prompt_raw", None)
+            out.append(b)
+        return out
+
+    model = SamModel(name)
+    model.init_weights(seed=0)
+    start = {k: v.float() for k, v in load_file(os.path.join(ROOT, "tests", "golden",
+                                                              "valdice_start_decoder.safetensors")).items()}
+    missing = set(start) - set(model.state_dict())
+    if missing:
+        raise RuntimeError(f"start decoder keys not in the model: {sorted(missing)[:3]}")
+    model.load_state_dict(start, strict=False)
+    model = model.to(device)
+    step = FusedTrainStep(model, lr=lr, topological=True, graphs=True, pipeline=True)
+
+    def run(seed, epochs, limit=None, evals=None):
+        k = 0
+        for ep in range(epochs):
+            tr = epoch_batches(seed, 128, ep)
+            for i, b in enumerate(tr):
+                if limit is not None and k >= limit:
+                    return
+                last = i + 1 == len(tr) or (limit is not None and k + 1 >= limit)
+                step.step(b, next_batch=None if last else tr[i + 1])
+                k += 1
+            if evals is not None:
+                evals.append(dice())
+
+    val = epoch_batches(3001, 32, 0)
+
+    def dice():
+        step.flush()
+        c = torch.zeros(14, 3, dtype=torch.int64)
+        for v in val:
+            c += class_confusion(predict_masks(model, v), v["gt_u8"], v["mask_values"])
+        return round(mean_dice(c), 5)
+
+    run(2000, 4, limit=64)
+    hip = [dice()]
+    run(2001, 4, evals=hip)
+    ora = gold["oracle_dice"]
+    diffs = [round(h - o, 5) for h, o in zip(hip, ora)]
+    out = {"steps": gold["steps"], "hip": hip, "oracle": ora, "diff": diffs,
+           "max_abs_diff": round(max(abs(d) for d in diffs), 5), "tolerance": 0.005,
+           "within": bool(max(abs(d) for d in diffs) <= 0.005), "seconds": round(time.perf_counter() - t0, 1),
+           "protocol": "tests/test_gpu_val_dice.py (warm start: 64 HIP steps; 4 epochs x 16 steps; 32 held-out scans)",
+           "oracle_source": "tests/golden/valdice_oracle.json"}
+    log(f"val protocol: {out}")
+    del step, model
+    torch.cuda.empty_cache()
+    return out
+
+
 def time_training_loop(args, device, n_images=128):
     """The drop-in loop itself (train.training, ref:octsam/models/training.py:184 -> training_utils.py:27-80) over a
     synthetic n_images-image epoch: its defaults (hipGraphs + encoder lookahead, HIP data path on a side stream),
@@ -686,7 +771,7 @@ def main():
         loop = time_training_loop(args, device, args.loop_images)
 
     log(f"rank {rank}: {dt * 1e3 / args.steps:.2f} ms/step")
-    val_dice = val_metrics = None
+    val_dice = val_metrics = val_proto = None
     if args.val and rank == 0:
         vb = data.to_device_batch(make_batch(argparse.Namespace(batch=args.val, prompt=args.prompt), 999, device,
                                              processor), device)
@@ -696,6 +781,8 @@ def main():
         acc = EvalAccumulator()
         acc.add(masks, vb["gt_u8"], vb["mask_values"])
         val_metrics = {k: round(v, 5) for k, v in acc.compute()["mean"].items()}
+    if args.val_protocol and rank == 0 and world == 1 and args.model == "facebook/sam-vit-base":
+        val_proto = val_protocol(args, device)
 
     data_path = None
     if args.data_path and rank == 0:
@@ -726,7 +813,8 @@ def main():
                         "step's decoder; each timed step runs its own encoder)" if pipe else "hipgraph")},
             "sequential_ms_per_step": None if seq_ms is None else round(seq_ms, 3),
             "loss_last_step": {"dice": loss_h[0], "ce": loss_h[1], "topo": loss_h[2], "total": loss_h[3]},
-            "val_dice": val_dice,
+            "val_dice_protocol": val_proto,
+            "val_dice_after_timed_steps": val_dice,
             "val_metrics_mean": val_metrics,
             "data_path": data_path,
             "value_end_to_end": e2e["value"] if e2e else None,

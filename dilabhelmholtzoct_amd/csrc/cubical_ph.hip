@@ -122,7 +122,7 @@ struct Smem {
     struct {  // dimension d's records at [rec_base(d), rec_base(d) + rec_cap(d))
       uint64_t key[REC0 + REC1];  // destroyer key (value bits << 32 | position / pixel)
       int c[REC0 + REC1];         // creator: cell position, then top-coface pixel
-      float cv[REC0 + REC1];      // creator value
+      double pers[REC0 + REC1];   // persistence (death - birth value, in double like gudhi), computed once
     } rec;
   } u;
   u16 vinv[MAXN];  // rank -> vertex id
@@ -187,6 +187,85 @@ __device__ void sort_keys(uint64_t* keys, int tid) {
   if (wave_phase) __syncthreads();
 }
 
+// Stable LSD radix sort (4-bit digits) of n <= NTHR * CMAX elements in LDS, ping-ponging between a and b; the
+// digits are bits [shift, shift + nbits) of each element (nbits % 4 == 0). Thread t owns the contiguous chunk
+// [t C, t C + C) (C = ceil(n / NTHR)) and the digit table (u16, 16 digits x NTHR threads, digit-major) is scanned in
+// that order, so equal digits keep their input order: stability makes a sort by value alone over position-ordered
+// input equal to the (value, position) sort of the bitonic form. Returns the buffer holding the result.
+// (Replaces two 8192-wide bitonic sorts: 415k of the kernel's 1.39M cycles, scripts/micro/ph_timing.hip.)
+template <typename T, int CMAX>
+__device__ T* radix_sort(T* a, T* b, int n, int shift, int nbits, uint16_t* tab, int* wtot, int tid) {
+  const int C = (n + NTHR - 1) / NTHR;
+  const int lo = min(n, tid * C), hi = min(n, lo + C);
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int sh = shift; sh < shift + nbits; sh += 4) {
+    T v[CMAX];
+    uint64_t c0 = 0, c1 = 0;  // 8-bit per-digit counters (C <= 16)
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) {
+      if (k < C && lo + k < hi) {
+        v[k] = a[lo + k];
+        const int d = (int)(v[k] >> sh) & 15;
+        if (d < 8) c0 += 1ull << (8 * d);
+        else c1 += 1ull << (8 * (d - 8));
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 16; ++d) tab[d * NTHR + tid] = (uint16_t)(((d < 8 ? c0 >> (8 * d) : c1 >> (8 * (d - 8)))) & 0xff);
+    __syncthreads();
+    // exclusive scan of the 16 * NTHR counts in digit-major order: thread t takes entries [16 t, 16 t + 16)
+    uint32_t e[16];
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      e[j] = run;
+      run += tab[16 * tid + j];
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += x;
+    }
+    if (lane == 63) wtot[wave] = (int)incl;
+    __syncthreads();
+    uint32_t base = incl - run;
+    for (int w = 0; w < wave; ++w) base += (uint32_t)wtot[w];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) tab[16 * tid + j] = (uint16_t)(base + e[j]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CMAX; ++k) {
+      if (k < C && lo + k < hi) {
+        const int d = (int)(v[k] >> sh) & 15;
+        const int pos = tab[d * NTHR + tid];
+        tab[d * NTHR + tid] = (uint16_t)(pos + 1);
+        b[pos] = v[k];
+      }
+    }
+    __syncthreads();
+    T* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// inclusive block scan of one int per thread (tid order)
+__device__ __forceinline__ int block_scan_incl(int x, int* wtot, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wtot[wave] = x;
+  __syncthreads();
+  for (int w = 0; w < wave; ++w) x += wtot[w];
+  __syncthreads();
+  return x;
+}
+
 // vertex id <-> bitmap position
 __device__ __forceinline__ int vert_pos(const Map& m, int vid) { return 2 * (vid % (m.W + 1)) + m.W2 * 2 * (vid / (m.W + 1)); }
 __device__ __forceinline__ int pos_vert(const Map& m, int pos) { return (pos % m.W2) / 2 + (m.W + 1) * ((pos / m.W2) / 2); }
@@ -235,7 +314,8 @@ __device__ void uf_wave(Smem& s, const Map& m, int ne, int npix) {
     }
     int my_young = -1, my_old = 0;
     // branch-free: an edge whose roots already agree relabels nothing (young == old) and is not recorded;
-    // the invalid tail lanes hold ru == rv == 0
+    // the invalid tail lanes hold ru == rv == 0 (walking only the lanes whose roots differ at the chunk start,
+    // an s_ff1 loop with a lane-indexed readlane, measured slower: 427 -> 493 us per launch)
 #pragma unroll 8
     for (int j = 0; j < 64; ++j) {
       const int sa = __builtin_amdgcn_readlane(ru, j);
@@ -275,59 +355,83 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     s.nrec[0] = s.nrec[1] = 0;
   }
   __syncthreads();
-  // 1. node filtration order: vertices (lower-star value, bitmap position) then pixels (value, index),
-  //    one sort; type bit 46 keeps the two lists apart
-  for (int i = tid; i < NP2; i += NTHR) {
-    uint64_t k = ~0ull;
-    if (i < nv) {
-      const int pos = vert_pos(m, i);
-      k = ((uint64_t)ord_bits(cell_value(m, pos)) << 14) | (uint32_t)pos;
-    } else if (i < nv + npix) {
-      const int px = i - nv;
-      k = (1ull << 46) | ((uint64_t)ord_bits(s.vals[px]) << 14) | (uint32_t)px;
-    }
-    s.keys[i] = k;
-  }
+  // radix scratch: the digit table and wave totals sit in the union past the union-find arrays (the pair records
+  // that share those bytes are built only after the union-find)
+  uint16_t* tab = (uint16_t*)((char*)&s.u + sizeof(s.u.uf));
+  int* wtot = (int*)(tab + 16 * NTHR);
   for (int i = tid; i <= npix; i += NTHR) s.u.uf.par[1][i] = (u16)i;
   for (int i = tid; i < nv; i += NTHR) s.u.uf.par[0][i] = (u16)i;
-  __syncthreads();
   PH_STAMP(1);
-  sort_keys(s.keys, tid);
-  for (int i = tid; i < nv + npix; i += NTHR) {
-    const int low = (int)(s.keys[i] & 0x3fff);
-    if (i < nv) {
-      const int vid = pos_vert(m, low);
-      s.vinv[i] = (u16)vid;
-      s.u.uf.vrank[vid] = (u16)i;
-    } else {
-      s.pinv[i - nv] = (u16)low;
-      s.u.uf.prank[low] = (u16)(i - nv);
-    }
-  }
+  // 1a. pixel order (value, index): stable radix sort of (ord(value) << 32 | px) over the index-ordered pixels
+  uint64_t* kp = s.keys;            // [0, 32 KB)
+  uint64_t* kq = s.keys + NP2 / 2;  // [32 KB, 64 KB)
+  for (int i = tid; i < npix; i += NTHR) kp[i] = ((uint64_t)ord_bits(s.vals[i]) << 32) | (uint32_t)i;
   __syncthreads();
-  // 2. edge (1-cell) order: (lower-star value, bitmap position) -> sorted positions epos
-  const int nh = (H + 1) * W, nvrt = H * (W + 1), ne = nh + nvrt;
-  for (int i = tid; i < NP2; i += NTHR) {
-    uint64_t k = ~0ull;
-    if (i < ne) {
-      int X, Y;
-      if (i < nh) { Y = 2 * (i / W); X = 2 * (i % W) + 1; }
-      else { int j = i - nh; Y = 2 * (j / (W + 1)) + 1; X = 2 * (j % (W + 1)); }
-      int pos = X + m.W2 * Y;
-      k = ((uint64_t)ord_bits(cell_value(m, pos)) << 32) | (uint32_t)pos;
-    }
-    s.keys[i] = k;
-  }
-  __syncthreads();
-  sort_keys(s.keys, tid);
+  const uint64_t* sp = radix_sort<uint64_t, MAX_PIX / NTHR>(kp, kq, npix, 32, 32, tab, wtot, tid);  // 8 passes: kp
+  // pixel ranks, and DENSE value ranks (equal values, equal rank; the node and edge values are pixel values, so
+  // their orders follow from these 12-bit ranks)
+  uint16_t* dr = (uint16_t*)(s.keys + NP2 - MAX_PIX / 4);  // [56 KB, 64 KB): kq is dead
   {
-    uint32_t ep[NP2 / NTHR];
-#pragma unroll
-    for (int t = 0; t < NP2 / NTHR; ++t) ep[t] = (uint32_t)s.keys[tid + t * NTHR];
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < NP2 / NTHR; ++t) ((uint32_t*)s.keys)[tid + t * NTHR] = ep[t];
+    const int C = (npix + NTHR - 1) / NTHR, lo = min(npix, tid * C), hi = min(npix, lo + C);
+    int f = 0;
+    for (int i = lo; i < hi; ++i) f += (i > 0 && (sp[i] >> 32) != (sp[i - 1] >> 32)) ? 1 : 0;
+    int r = block_scan_incl(f, wtot, tid) - f;  // distinct-value steps before this chunk
+    for (int i = lo; i < hi; ++i) {
+      r += (i > 0 && (sp[i] >> 32) != (sp[i - 1] >> 32)) ? 1 : 0;
+      const int px = (int)(sp[i] & 0xffff);
+      dr[px] = (uint16_t)r;
+      s.pinv[i] = (u16)px;
+      s.u.uf.prank[px] = (u16)i;
+    }
   }
+  __syncthreads();
+  // 1b. vertex order (value, position): vertex ids are position-ordered, so a stable sort by the dense rank of
+  //     the vertex's lower-star value (the minimum over its <= 4 pixels) gives it
+  uint32_t* va = (uint32_t*)s.keys;          // [0, 17 KB)
+  uint32_t* vb = (uint32_t*)s.keys + MAXN;   // [17 KB, 34 KB)
+  for (int i = tid; i < nv; i += NTHR) {
+    const int vy = i / (W + 1), vx = i - vy * (W + 1);
+    int r = 0xffff;
+    for (int py = max(vy - 1, 0); py <= min(vy, H - 1); ++py)
+      for (int px = max(vx - 1, 0); px <= min(vx, W - 1); ++px) r = min(r, (int)dr[py * W + px]);
+    va[i] = ((uint32_t)r << 16) | (uint32_t)i;
+  }
+  __syncthreads();
+  const uint32_t* sv = radix_sort<uint32_t, (MAXN + NTHR - 1) / NTHR>(va, vb, nv, 16, 12, tab, wtot, tid);  // -> vb
+  for (int i = tid; i < nv; i += NTHR) {
+    const int vid = (int)(sv[i] & 0xffff);
+    s.vinv[i] = (u16)vid;
+    s.u.uf.vrank[vid] = (u16)i;
+  }
+  __syncthreads();
+  // 2. edge (1-cell) order (value, bitmap position): the edges in raster position order (even rows: the W
+  //    horizontal edges at odd X; odd rows: the W + 1 vertical edges at even X), stably sorted by the dense rank
+  //    of their lower-star value -> sorted positions epos (u32 at s.keys, as the union-find reads them)
+  const int nh = (H + 1) * W, nvrt = H * (W + 1), ne = nh + nvrt;
+  uint32_t* ea = (uint32_t*)s.keys;        // [0, 32 KB): the input (dr, at [56 KB, 64 KB), is read meanwhile)
+  uint32_t* eb = (uint32_t*)s.keys + NP2;  // [32 KB, 64 KB): 3 passes end here
+  for (int i = tid; i < ne; i += NTHR) {
+    const int r2 = i / (2 * W + 1), rem = i - r2 * (2 * W + 1);
+    int r;
+    int pos;
+    if (rem < W) {  // horizontal edge: row Y = 2 r2, X = 2 rem + 1; pixels above / below in column rem
+      const int Y = 2 * r2, X = 2 * rem + 1;
+      pos = X + m.W2 * Y;
+      r = 0xffff;
+      if (r2 > 0) r = min(r, (int)dr[(r2 - 1) * W + rem]);
+      if (r2 < H) r = min(r, (int)dr[r2 * W + rem]);
+    } else {  // vertical edge: row Y = 2 r2 + 1, X = 2 (rem - W); pixels left / right in row r2
+      const int c = rem - W, Y = 2 * r2 + 1, X = 2 * c;
+      pos = X + m.W2 * Y;
+      r = 0xffff;
+      if (c > 0) r = min(r, (int)dr[r2 * W + c - 1]);
+      if (c < W) r = min(r, (int)dr[r2 * W + c]);
+    }
+    ea[i] = ((uint32_t)r << 14) | (uint32_t)pos;
+  }
+  __syncthreads();
+  const uint32_t* se = radix_sort<uint32_t, NP2 / NTHR>(ea, eb, ne, 14, 12, tab, wtot, tid);  // 3 passes: eb
+  for (int i = tid; i < ne; i += NTHR) ea[i] = se[i] & 0x3fff;  // positions to [0, 32 KB); the merge logs follow
   __syncthreads();
   const int wave = tid >> 6;
   PH_STAMP(2);
@@ -402,7 +506,7 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     for (int i = tid; i < n; i += NTHR) {
       const int c = top_coface(m, s.u.rec.c[o + i]);
       s.u.rec.c[o + i] = c;
-      s.u.rec.cv[o + i] = s.vals[c];
+      s.u.rec.pers[o + i] = (double)unord_bits((uint32_t)(s.u.rec.key[o + i] >> 32)) - (double)s.vals[c];
     }
   }
   __syncthreads();
@@ -422,12 +526,12 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     for (int i = tid; i < n; i += NTHR) {
       const uint64_t ki = s.u.rec.key[o + i];
       const int ci = s.u.rec.c[o + i];
-      const double pi = (double)unord_bits((uint32_t)(ki >> 32)) - (double)s.u.rec.cv[o + i];
+      const double pi = s.u.rec.pers[o + i];
       int rank = 0;
+#pragma unroll 4
       for (int j = 0; j < n; ++j) {
-        const uint64_t kj = s.u.rec.key[o + j];
-        const double pj = (double)unord_bits((uint32_t)(kj >> 32)) - (double)s.u.rec.cv[o + j];
-        rank += (pj > pi) || (pj == pi && kj < ki);
+        const double pj = s.u.rec.pers[o + j];
+        rank += (pj > pi) || (pj == pi && s.u.rec.key[o + j] < ki);
       }
       if (rank < max_pairs) {
         const int pos = (int)(uint32_t)ki;
@@ -450,7 +554,7 @@ extern "C" int octsam_cubical_ph(const float* maps, int32_t nmaps, int32_t H, in
   OCTSAM_CHECK_ARG(maps && pairs0 && pairs1 && essential && counts, "octsam_cubical_ph: null pointer");
   OCTSAM_CHECK_ARG(nmaps >= 0 && H >= 1 && W >= 1 && max_pairs >= 1, "octsam_cubical_ph: bad sizes");
   OCTSAM_CHECK_ARG(H * W <= MAX_PIX && (H + 1) * W + H * (W + 1) <= NP2 && (H + 1) * (W + 1) + H * W <= NP2 &&
-                       (2 * W + 1) * (2 * H + 1) <= 16384,
+                       (2 * W + 1) * (2 * H + 1) <= 16384 && (H + 1) * (W + 1) <= MAXN,
                    "octsam_cubical_ph: map %dx%d too large (<= 63x63)", H, W);
   if (nmaps == 0) return 0;
   hipLaunchKernelGGL(cubical_ph_kernel, dim3(nmaps), dim3(NTHR), 0, (hipStream_t)stream, maps, H, W, max_pairs,

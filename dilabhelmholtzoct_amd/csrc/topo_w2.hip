@@ -13,8 +13,9 @@
 //     its argmin takes the lowest column index among equal minima — the host loop's first strict minimum;
 //   * the transport cost is summed in the host's order by one lane; per entry the costs are summed in map
 //     order, rounded to float, and the gradient is scattered into the map's row in LDS with the host's
-//     per-pixel addition order (creators, then destroyers): one thread per contribution, a pixel hit several
-//     times summed in that order by the thread of its first contribution; the row written out by the workgroup;
+//     per-pixel addition order (creators, then destroyers): every contribution computed once by its own thread
+//     into LDS, a pixel hit several times summed in that order by the thread of its first contribution; the row
+//     written out by the workgroup;
 //   * no FMA contraction anywhere (the host build has none).
 // Bit-identity holds for q = 2 (the call site's loss_q: **2 is one fp32 multiply, the 1/q power a
 // correctly rounded sqrt on both sides); other q use pow on both sides (device ocml vs host libm may
@@ -272,11 +273,17 @@ __global__ void __launch_bounds__(256) w2_loss_kernel(const int32_t* __restrict_
     for (int i = t; i < nvals; i += 256) out[i] = __builtin_nanf("");
     return;
   }
+  // LDS: row[nvals] (the gradient row), hits[nvals] (contributions per pixel), first[nvals] (lowest contribution
+  // index o per pixel), pix[2n] / cval[2n] (each contribution's pixel and value, computed once in parallel)
   float* row = (float*)w2_smem;
-  int* hits = (int*)(row + nvals);  // contributions per pixel
+  int* hits = (int*)(row + nvals);
+  int* first = hits + nvals;
+  int* pix = first + nvals;
+  float* cval = (float*)(pix + 2 * max_pairs);
   for (int i = t; i < nvals; i += 256) {
     row[i] = 0.0f;
     hits[i] = 0;
+    first[i] = 0x7fffffff;
   }
   __syncthreads();
   const int e = map_entry[k];
@@ -286,15 +293,17 @@ __global__ void __launch_bounds__(256) w2_loss_kernel(const int32_t* __restrict_
   const float* v1 = vals + (size_t)k * nvals;
   const float* v2 = vals + (size_t)(Kn + k) * nvals;
   const int32_t* mk = match + (size_t)k * max_pairs;
-  // The host adds the 2n contributions in the order o = pass * n + i (creators, then destroyers) into a zeroed
-  // row. Here thread o computes contribution o; a pixel hit once gets 0 + c, a pixel hit several times is summed
-  // by the thread of its first contribution, in o order — the same fp32 additions, so the row is bit-identical.
-  for (int o = t; o < 2 * n; o += 256) atomicAdd(&hits[p1[2 * (o % n) + o / n]], 1);
   float scale = 0.0f;
   if (n > 0) scale = (float)(lamda / n_entries * w2_droot(entry_tot(e), q));
-  __syncthreads();
-  auto contrib = [&](int o) -> float {
+  // The host adds the 2n contributions in the order o = pass * n + i (creators, then destroyers) into a zeroed
+  // row. Here every contribution is computed once (thread o), its pixel counted and the pixel's lowest o kept
+  // (LDS atomics: a count and a minimum, order-independent); a pixel hit once gets 0 + c, a pixel hit several
+  // times is summed in o order by the thread of its lowest o, from LDS -- the same fp32 additions, so the row is
+  // bit-identical to the host's. (Round 3 / the first parallel form re-read the pair lists from global memory in
+  // per-contribution serial loops: 235-246 us per launch.)
+  for (int o = t; o < 2 * n; o += 256) {
     const int i = o % n, pass = o / n;
+    const int px = p1[2 * i + pass];
     const int j = mk[i];
     const float d1p[2] = {v1[p1[2 * i]], v1[p1[2 * i + 1]]};
     float d2p[2] = {0.0f, 0.0f};
@@ -304,20 +313,36 @@ __global__ void __launch_bounds__(256) w2_loss_kernel(const int32_t* __restrict_
     }
     float g0, g1;
     w2_grad_point(d1p, d2p, 0, j >= 0 ? 0 : -1, q, &g0, &g1);
-    return scale * (pass == 0 ? g0 : g1);
-  };
+    pix[o] = px;
+    cval[o] = scale * (pass == 0 ? g0 : g1);
+    atomicAdd(&hits[px], 1);
+    atomicMin(&first[px], o);
+  }
+  __syncthreads();
   for (int o = t; o < 2 * n; o += 256) {
-    const int px = p1[2 * (o % n) + o / n];
+    const int px = pix[o];
+    if (first[px] != o) continue;
     if (hits[px] == 1) {
-      row[px] = 0.0f + contrib(o);
+      row[px] = 0.0f + cval[o];
       continue;
     }
-    bool first = true;
-    for (int x = 0; x < o && first; ++x) first = p1[2 * (x % n) + x / n] != px;
-    if (!first) continue;
+    // the pixel's other contributions, in o order: scanned 8 at a time (independent LDS reads in flight), stopping
+    // once all hits[px] of them are summed
     float acc = 0.0f;
-    for (int x = o; x < 2 * n; ++x)
-      if (p1[2 * (x % n) + x / n] == px) acc += contrib(x);
+    const int want = hits[px];
+    int got = 0;
+    for (int x0 = o; x0 < 2 * n && got < want; x0 += 8) {
+      int pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pv[u] = x0 + u < 2 * n ? pix[x0 + u] : -1;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (pv[u] == px) {
+          acc += cval[x0 + u];
+          ++got;
+        }
+      }
+    }
     row[px] = acc;
   }
   __syncthreads();
@@ -350,8 +375,9 @@ extern "C" int octsam_topo_w2(const int32_t* pairs, const int32_t* cnt, const fl
   OCTSAM_CHECK_ARG(workspace_bytes >= octsam_topo_w2_workspace(Kn, max_pairs),
                    "octsam_topo_w2: workspace of %lld bytes, need %lld", (long long)workspace_bytes,
                    (long long)octsam_topo_w2_workspace(Kn, max_pairs));
-  OCTSAM_CHECK_ARG((size_t)nvals * 8 <= 65536, "octsam_topo_w2: nvals %d above the 64 KB gradient row + hit counts",
-                   nvals);
+  const size_t grad_lds = (size_t)nvals * 12 + (size_t)max_pairs * 16;  // row, hits, first + pix, cval (w2_loss)
+  OCTSAM_CHECK_ARG(grad_lds <= 160 * 1024, "octsam_topo_w2: nvals %d / max_pairs %d need %zu B of LDS (> 160 KB)",
+                   nvals, max_pairs, grad_lds);
   hipStream_t s = (hipStream_t)stream;
   const W2Layout L(max_pairs);
   int dev = 0, lds_max = 0;
@@ -375,7 +401,14 @@ extern "C" int octsam_topo_w2(const int32_t* pairs, const int32_t* cnt, const fl
   w2_map_kernel<<<Kn, W2_THREADS, lds ? L.bytes : 0, s>>>(pairs, cnt, vals, Kn, max_pairs, nvals, feat_col, q, costs,
                                                            match, status, gscratch, lds ? 1 : 0);
   OCTSAM_LAUNCH_CHECK("octsam_topo_w2 (transport)");
-  w2_loss_kernel<<<Kn + 1, 256, want_grad ? (size_t)nvals * 8 : 0, s>>>(
+  if (want_grad && grad_lds > 65536) {
+    static size_t attr_loss = 0;
+    if (grad_lds > attr_loss) {
+      (void)hipFuncSetAttribute((const void*)w2_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grad_lds);
+      attr_loss = grad_lds;
+    }
+  }
+  w2_loss_kernel<<<Kn + 1, 256, want_grad ? grad_lds : 0, s>>>(
       pairs, cnt, vals, Kn, max_pairs, nvals, feat_col, q, lamda, entry_maps, entry_off, map_entry, n_entries, costs,
       match, status, want_grad, loss_out, dpred);
   OCTSAM_LAUNCH_CHECK("octsam_topo_w2 (loss)");
