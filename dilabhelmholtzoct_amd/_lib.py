@@ -121,6 +121,15 @@ _SIGNATURES = {
                                        ctypes.c_double, c_void_p, c_void_p]),
     "octsam_postproc_bwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_dicece_pp_rows": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float,
+                                        c_float, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
+    "octsam_pp_bwd_rows_maps": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p]),
+    "octsam_pp_bwd_cols": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+    "octsam_topo_bwd_compact": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                          c_void_p, c_float, c_void_p, c_void_p]),
     "octsam_topo_down": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                    c_int32, c_void_p, c_void_p, c_void_p]),
     "octsam_topo_bwd": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

@@ -419,6 +419,129 @@ __global__ __launch_bounds__(256) void pp_bwd_cols_kernel(const float* __restric
   dlow[(long long)m * S * S + e] = acc;
 }
 
+// DiceCE backward fused with the post-processing adjoint's row pass (the 170 MB d-mask write + read of the two-kernel
+// form): one workgroup per (image b, output row i) computes d(DiceCE)/d mask for the row's pixels of all N prompts
+// (dicece_bwd_kernel's per-pixel arithmetic: the CE couples the N prompts at a pixel, so one workgroup holds all of
+// them) into LDS, adds the row's CE partial, and runs the row pass tmp[m][i][c] = sum_{(j,w) in colcsr[c]} w d[m][j]
+// for every map m = b N + n with keep[m] < 0 (thread c: one output column, its taps walked once for all N maps).
+// A map with keep[m] = k >= 0 (the topological loss's maps: their topo gradient joins later) gets its d-mask row
+// written to dkeep[k] instead; octsam_topo_bwd_compact and octsam_pp_bwd_rows_maps finish it.
+template <int NR>
+__global__ __launch_bounds__(128) void dicece_pp_rows_kernel(const float* __restrict__ x, const uint8_t* __restrict__ gt,
+                                                             const float* __restrict__ coef, int N, int H, int W,
+                                                             float w_dice, float w_ce, float inv_bhw, int S,
+                                                             const int* __restrict__ cptr, const int* __restrict__ cidx,
+                                                             const float* __restrict__ cw, const int* __restrict__ keep,
+                                                             float* __restrict__ dkeep, float* __restrict__ tmp,
+                                                             double* __restrict__ ce_part) {
+  // 128 threads x 4 consecutive pixels (16-B logit loads, 4-B target loads: dicece_bwd4_kernel's access pattern)
+  extern __shared__ float dm[];  // [N][W]
+  const int i = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const long long HW = (long long)H * W;
+  const long long row0 = (long long)b * N * HW + (long long)i * W;  // (b, n = 0, i, 0)
+  const float* cfb = coef + 2 * b * N;
+  int kp[NR];
+#pragma unroll
+  for (int n = 0; n < NR; ++n) kp[n] = (n < N && keep) ? keep[b * N + n] : -1;
+  double ce = 0.0;
+  for (int j0 = 4 * tid; j0 < W; j0 += 4 * 128) {
+    float4 xv[NR];
+    uint32_t tv[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      if (n < N) {
+        xv[n] = *(const float4*)(x + row0 + n * HW + j0);
+        tv[n] = *(const uint32_t*)(gt + row0 + n * HW + j0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        if (n < N) mx = fmaxf(mx, ((const float*)&xv[n])[k]);
+      float se = 0.0f, tsum = 0.0f, tx = 0.0f;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          const float xk = ((const float*)&xv[n])[k], tk = (float)((tv[n] >> (8 * k)) & 0xFF);
+          se += __expf(xk - mx);
+          tsum += tk;
+          tx += tk * xk;
+        }
+      }
+      const float lse = mx + __logf(se);
+      ce += (double)(lse * tsum - tx);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < N) {
+          const float xk = ((const float*)&xv[n])[k], tk = (float)((tv[n] >> (8 * k)) & 0xFF);
+          const float sm = __expf(xk - lse);
+          const float p = 1.0f / (1.0f + __expf(-xk));
+          const float gd = (cfb[2 * n] * tk + cfb[2 * n + 1]) * p * (1.0f - p);
+          const float gc = (sm * tsum - tk) * inv_bhw;
+          ((float*)&xv[n])[k] = w_dice * gd + w_ce * gc;  // the logit is dead: its register takes d
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      if (n < N) {
+        if (kp[n] >= 0) *(float4*)(dkeep + (long long)kp[n] * HW + (long long)i * W + j0) = xv[n];
+        else *(float4*)(dm + n * W + j0) = xv[n];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < S; c += 128) {
+    float acc[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[n] = 0.0f;
+    for (int e = cptr[c]; e < cptr[c + 1]; ++e) {
+      const int j = cidx[e];
+      const float wv = cw[e];
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+        if (n < N) acc[n] += wv * dm[n * W + j];
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      if (n < N && kp[n] < 0) tmp[((long long)(b * N + n) * H + i) * S + c] = acc[n];
+    }
+  }
+  __shared__ double red[2];
+  ce = wave_sum_d(ce);
+  if ((tid & 63) == 0) red[tid >> 6] = ce;
+  __syncthreads();
+  if (tid == 0) ce_part[(long long)b * H + i] = red[0] + red[1];
+}
+
+// the row pass for maps given in compact storage: dout[k] (k < K) -> tmp[map_idx[k]] (pp_bwd_rows_kernel's order)
+__global__ __launch_bounds__(256) void pp_bwd_rows_maps_kernel(const float* __restrict__ dout, const int* __restrict__ map_idx,
+                                                               int oh, int ow, int S, const int* __restrict__ cptr,
+                                                               const int* __restrict__ cidx, const float* __restrict__ cw,
+                                                               float* __restrict__ tmp) {
+  __shared__ float rows[4][1024];
+  const int k = blockIdx.y, i0 = blockIdx.x * 4, tid = threadIdx.x;
+  const int m = map_idx[k];
+  const int nr = min(4, oh - i0);
+  for (int e = tid; e < nr * ow; e += 256) {
+    const int r = e / ow, j = e - r * ow;
+    rows[r][j] = dout[((long long)k * oh + i0 + r) * ow + j];
+  }
+  __syncthreads();
+  for (int b = tid; b < S; b += 256) {
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int e = cptr[b]; e < cptr[b + 1]; ++e) {
+      const int j = cidx[e];
+      const float wv = cw[e];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] += wv * rows[r][j];
+    }
+    for (int r = 0; r < nr; ++r) tmp[((long long)m * oh + i0 + r) * S + b] = acc[r];
+  }
+}
+
 // topo forward: pred50[k] = interp_ac(sigmoid(masks[map_idx[k]])), gt50[k] = interp_ac(gt[map_idx[k]])
 __global__ __launch_bounds__(256) void topo_down_kernel(const float* __restrict__ masks, const uint8_t* __restrict__ gt,
                                                         const int* __restrict__ map_idx, int ih, int iw, int oh, int ow,
@@ -443,10 +566,11 @@ __global__ __launch_bounds__(256) void topo_down_kernel(const float* __restrict_
 }
 
 // topo backward: dmask[map_idx[k]] += d(interp_ac o sigmoid)^T dpred[k]
+// compact: dmask holds the K maps themselves ([K, ih, iw]; masks are still read at map_idx[k])
 __global__ __launch_bounds__(256) void topo_bwd_kernel(const float* __restrict__ masks, const int* __restrict__ map_idx,
                                                        int ih, int iw, int oh, int ow, float sh, float sw, int sig,
                                                        const float* __restrict__ dpred, float scale,
-                                                       float* __restrict__ dmask) {
+                                                       float* __restrict__ dmask, int compact) {
   const int k = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= oh * ow) return;
@@ -454,15 +578,16 @@ __global__ __launch_bounds__(256) void topo_bwd_kernel(const float* __restrict__
   if (g == 0.0f) return;
   const int i = e / ow, j = e % ow;
   const long long mo = (long long)map_idx[k] * ih * iw;
+  const long long md = compact ? (long long)k * ih * iw : mo;
   Lin a = lin_act(i, ih, sh), b = lin_act(j, iw, sw);
   auto add = [&](int r, int c, float w) {
-    long long idx = mo + (long long)r * iw + c;
+    const long long off = (long long)r * iw + c;
     float d = 1.0f;
     if (sig) {
-      float s = 1.0f / (1.0f + __expf(-masks[idx]));
+      float s = 1.0f / (1.0f + __expf(-masks[mo + off]));
       d = s * (1.0f - s);
     }
-    atomicAdd(dmask + idx, g * w * d);
+    atomicAdd(dmask + md + off, g * w * d);
   };
   add(a.i0, b.i0, a.l0 * b.l0);
   add(a.i0, b.i1, a.l0 * b.l1);
@@ -605,7 +730,77 @@ extern "C" int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32
   if (K == 0) return 0;
   float sh = (float)(in_h - 1) / (float)(out_h - 1), sw = (float)(in_w - 1) / (float)(out_w - 1);
   hipLaunchKernelGGL(topo_bwd_kernel, dim3((out_h * out_w + 255) / 256, K), dim3(256), 0, (hipStream_t)stream, masks,
-                     map_idx, in_h, in_w, out_h, out_w, sh, sw, apply_sigmoid, dpred, scale, dmask);
+                     map_idx, in_h, in_w, out_h, out_w, sh, sw, apply_sigmoid, dpred, scale, dmask, 0);
   OCTSAM_LAUNCH_CHECK("octsam_topo_bwd");
+  return 0;
+}
+
+extern "C" int octsam_topo_bwd_compact(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h,
+                                       int32_t in_w, int32_t out_h, int32_t out_w, int32_t apply_sigmoid,
+                                       const float* dpred, float scale, float* dmask_k, void* stream) {
+  OCTSAM_CHECK_ARG(masks && map_idx && dpred && dmask_k && K >= 0, "octsam_topo_bwd_compact: bad args");
+  if (K == 0) return 0;
+  float sh = (float)(in_h - 1) / (float)(out_h - 1), sw = (float)(in_w - 1) / (float)(out_w - 1);
+  hipLaunchKernelGGL(topo_bwd_kernel, dim3((out_h * out_w + 255) / 256, K), dim3(256), 0, (hipStream_t)stream, masks,
+                     map_idx, in_h, in_w, out_h, out_w, sh, sw, apply_sigmoid, dpred, scale, dmask_k, 1);
+  OCTSAM_LAUNCH_CHECK("octsam_topo_bwd_compact");
+  return 0;
+}
+
+extern "C" int octsam_dicece_pp_rows(const float* masks, const uint8_t* gt, const float* coef, int32_t B, int32_t N,
+                                     int32_t H, int32_t W, float w_dice, float w_ce, int32_t S, const int32_t* col_ptr,
+                                     const int32_t* col_idx, const float* col_w, const int32_t* keep, float* dkeep,
+                                     float* tmp, double* ce_part, void* stream) {
+  OCTSAM_CHECK_ARG(masks && gt && coef && col_ptr && col_idx && col_w && tmp && ce_part && B > 0 && N > 0 && H > 0 &&
+                       W > 0 && S > 0 && (!keep || dkeep) && B <= 65535,
+                   "octsam_dicece_pp_rows: bad args");
+  OCTSAM_CHECK_ARG(N <= 32 && (size_t)N * W * 4 <= 160 * 1024 && (long long)B * H * W < (1LL << 31) && W % 4 == 0 &&
+                       ((uintptr_t)masks & 15) == 0 && ((uintptr_t)gt & 3) == 0 && (!dkeep || ((uintptr_t)dkeep & 15) == 0),
+                   "octsam_dicece_pp_rows: needs N <= 32 prompts, N * W * 4 <= 160 KB, W %% 4 == 0 and 16-B aligned "
+                   "masks / dkeep (N=%d, W=%d)", N, W);
+  const float inv = (float)(1.0 / ((double)B * H * W));
+  const size_t lds = (size_t)N * W * 4;
+  hipStream_t s = (hipStream_t)stream;
+  if (N <= 24) {
+    static size_t attr = 0;
+    if (lds > 65536 && lds > attr) {
+      (void)hipFuncSetAttribute((const void*)dicece_pp_rows_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr = lds;
+    }
+    hipLaunchKernelGGL(dicece_pp_rows_kernel<24>, dim3(H, B), dim3(128), lds, s, masks, gt, coef, N, H, W, w_dice, w_ce,
+                       inv, S, col_ptr, col_idx, col_w, keep, dkeep, tmp, ce_part);
+  } else {
+    static size_t attr = 0;
+    if (lds > 65536 && lds > attr) {
+      (void)hipFuncSetAttribute((const void*)dicece_pp_rows_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr = lds;
+    }
+    hipLaunchKernelGGL(dicece_pp_rows_kernel<32>, dim3(H, B), dim3(128), lds, s, masks, gt, coef, N, H, W, w_dice, w_ce,
+                       inv, S, col_ptr, col_idx, col_w, keep, dkeep, tmp, ce_part);
+  }
+  OCTSAM_LAUNCH_CHECK("octsam_dicece_pp_rows");
+  return 0;
+}
+
+extern "C" int octsam_pp_bwd_rows_maps(const float* dout_k, const int32_t* map_idx, int32_t K, int32_t S, int32_t out_h,
+                                       int32_t out_w, const int32_t* col_ptr, const int32_t* col_idx, const float* col_w,
+                                       float* tmp, void* stream) {
+  OCTSAM_CHECK_ARG(dout_k && map_idx && col_ptr && col_idx && col_w && tmp && K >= 0 && out_w <= 1024 && K <= 65535,
+                   "octsam_pp_bwd_rows_maps: bad args");
+  if (K == 0) return 0;
+  hipLaunchKernelGGL(pp_bwd_rows_maps_kernel, dim3((unsigned)((out_h + 3) / 4), K), dim3(256), 0, (hipStream_t)stream,
+                     dout_k, map_idx, out_h, out_w, S, col_ptr, col_idx, col_w, tmp);
+  OCTSAM_LAUNCH_CHECK("octsam_pp_bwd_rows_maps");
+  return 0;
+}
+
+extern "C" int octsam_pp_bwd_cols(const float* tmp, int32_t M, int32_t S, int32_t out_h, const int32_t* row_ptr,
+                                  const int32_t* row_idx, const float* row_w, float* dlowres, void* stream) {
+  OCTSAM_CHECK_ARG(tmp && row_ptr && row_idx && row_w && dlowres && M > 0 && M <= 65535, "octsam_pp_bwd_cols: bad args");
+  hipLaunchKernelGGL(pp_bwd_cols_kernel, dim3((S * S + 255) / 256, M), dim3(256), 0, (hipStream_t)stream, tmp, out_h, S,
+                     row_ptr, row_idx, row_w, dlowres);
+  OCTSAM_LAUNCH_CHECK("octsam_pp_bwd_cols");
   return 0;
 }

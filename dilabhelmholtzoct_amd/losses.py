@@ -145,6 +145,61 @@ def dicece_forward_backward(masks: torch.Tensor, gt_u8: torch.Tensor, dice_part:
     return loss, dmask
 
 
+_KEEP: dict = {}
+
+
+def _keep_table(B: int, N: int, maps, device):
+    """keep [B*N] int32: position k of map m in the topological loss's map list, else -1 (cached: fixed address for
+    captured graphs)."""
+    key = (B, N, tuple(maps), str(device))
+    if key not in _KEEP:
+        keep = torch.full((B * N,), -1, dtype=torch.int32)
+        for k, m in enumerate(maps):
+            keep[m] = k
+        _KEEP[key] = keep.to(device)
+    return _KEEP[key]
+
+
+def dicece_pp_rows(masks: torch.Tensor, gt_u8: torch.Tensor, dice_part: torch.Tensor, crop, *, maps=(),
+                   w_dice: float = 1.0, w_ce: float = 1.0, S: int = 256):
+    """The DiceCE loss and its backward fused with the post-processing adjoint's row pass (octsam_dicece_pp_rows):
+    no [B, N, H, W] d-mask in HBM. Returns (loss double [3] = dice, ce, total; tmp fp32 [B*N, H, S] (the row pass of
+    every map not in `maps`); dkeep fp32 [len(maps), H, W] (the d-mask of the topological loss's maps, whose topo
+    gradient joins in pp_rows_finish) or None). dice_part from postproc_forward with gt (training_utils.py:56-62)."""
+    B, N, H, W = masks.shape
+    M = B * N
+    dev = masks.device
+    dice_map = torch.empty(M, device=dev, dtype=torch.float64)
+    coef = torch.empty(M, 2, device=dev, dtype=torch.float32)
+    _lib.call("octsam_dice_reduce", K.ptr(dice_part), M, dice_part.shape[1], K.ptr(dice_map), K.ptr(coef))
+    cptr, cidx, cw_, _, _, _ = pp_tables(S, 1024, crop[0], crop[1], H, W, dev)
+    tmp = torch.empty(M, H, S, device=dev, dtype=torch.float32)
+    keep = _keep_table(B, N, maps, dev) if maps else None
+    dkeep = torch.empty(len(maps), H, W, device=dev, dtype=torch.float32) if maps else None
+    ce_part = torch.empty(B * H, device=dev, dtype=torch.float64)
+    _lib.call("octsam_dicece_pp_rows", K.ptr(masks), K.ptr(gt_u8), K.ptr(coef), B, N, H, W, w_dice, w_ce, S,
+              K.ptr(cptr), K.ptr(cidx), K.ptr(cw_), K.ptr(keep), K.ptr(dkeep), K.ptr(tmp), K.ptr(ce_part))
+    loss = torch.empty(3, device=dev, dtype=torch.float64)
+    _lib.call("octsam_loss_finalize", K.ptr(dice_map), M, K.ptr(ce_part), B * H, B, H * W, w_dice, w_ce, K.ptr(loss))
+    return loss, tmp, dkeep
+
+
+def pp_rows_finish(tmp: torch.Tensor, crop, orig, *, dkeep: torch.Tensor | None = None,
+                   midx: torch.Tensor | None = None, S: int = 256) -> torch.Tensor:
+    """Second half of the fused post-processing adjoint: the row pass of the kept maps (dkeep -> tmp[midx]) and the
+    column pass of every map -> d low-res masks fp32 [B*N, S, S]."""
+    M, H, _ = tmp.shape
+    W = orig[1]
+    dev = tmp.device
+    cptr, cidx, cw_, rptr, ridx, rw = pp_tables(S, 1024, crop[0], crop[1], H, W, dev)
+    if dkeep is not None and dkeep.shape[0]:
+        _lib.call("octsam_pp_bwd_rows_maps", K.ptr(dkeep), K.ptr(midx), dkeep.shape[0], S, H, W, K.ptr(cptr),
+                  K.ptr(cidx), K.ptr(cw_), K.ptr(tmp))
+    dlow = torch.empty(M, S, S, device=dev, dtype=torch.float32)
+    _lib.call("octsam_pp_bwd_cols", K.ptr(tmp), M, S, H, K.ptr(rptr), K.ptr(ridx), K.ptr(rw), K.ptr(dlow))
+    return dlow
+
+
 def _dice_partials(masks, gt_u8, nblk=64):
     """Dice partial sums of an already post-processed fp32 mask tensor (drop-in path): octsam_dice_partials."""
     B, N, H, W = masks.shape
@@ -342,12 +397,13 @@ def topo_host(pairs_h: np.ndarray, cnt_h: np.ndarray, vals_h: np.ndarray, entrie
 
 
 def topo_device_backward(masks: torch.Tensor, midx: torch.Tensor, dp: torch.Tensor, dmask: torch.Tensor, *,
-                         interp=50, logits=True):
-    """dmask += d topo / d masks, given d topo / d (resampled sigmoid map) dp [Kn, side^2] (capturable)."""
+                         interp=50, logits=True, compact=False):
+    """dmask += d topo / d masks, given d topo / d (resampled sigmoid map) dp [Kn, side^2] (capturable).
+    compact: dmask is [Kn, H, W], the Kn maps themselves (dicece_pp_rows' dkeep)."""
     B, N, H, W = masks.shape
     oh, ow = (interp, interp) if interp else (H, W)
-    _lib.call("octsam_topo_bwd", K.ptr(masks), K.ptr(midx), midx.numel(), H, W, oh, ow, int(logits),
-              K.ptr(dp), 1.0, K.ptr(dmask))
+    _lib.call("octsam_topo_bwd_compact" if compact else "octsam_topo_bwd", K.ptr(masks), K.ptr(midx), midx.numel(),
+              H, W, oh, ow, int(logits), K.ptr(dp), 1.0, K.ptr(dmask))
 
 
 def total_persistence_host(pairs_h, cnt_h, vals_h, entries, maps, *, col, q, lamda, dpred=None):

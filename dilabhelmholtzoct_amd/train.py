@@ -21,8 +21,8 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .losses import (dicece_forward_backward, postproc_backward, postproc_forward, topo_device_backward,
-                     topo_device_forward, topo_host, topo_index, topo_w2_device)
+from .losses import (dicece_forward_backward, dicece_pp_rows, postproc_backward, postproc_forward, pp_rows_finish,
+                     topo_device_backward, topo_device_forward, topo_host, topo_index, topo_w2_device)
 from .model import SamModel
 
 
@@ -95,6 +95,9 @@ class FusedTrainStep:
         # 17.04 vs 17.13 ms/step — the 16-workgroup persistence kernel beside the DiceCE backward delays it more
         # than it gains)
         self.fork_topo = False
+        # DiceCE backward fused with the post-processing adjoint's row pass (no [B, N, H, W] d-mask round trip;
+        # False: the round-3 octsam_dicece_bwd + octsam_postproc_bwd path, for A/B)
+        self.fused_pp = True
         self._parity = {}       # pixel shape -> parity of the graph sets the next step of that shape uses
         self._esets = {}        # (pixel shape, dtype, parity) -> captured encoder graph E
 
@@ -149,7 +152,7 @@ class FusedTrainStep:
         B, N, H, W = st.masks.shape
         job = getattr(st, "w2_job", None)
         if job is None:
-            st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
+            self._dicece(st)
             return
         entries, maps, midx, want_grad, diagrams = job
         main = torch.cuda.current_stream()
@@ -164,12 +167,24 @@ class FusedTrainStep:
                 pairs, cnt, vals = diagrams
             st.topo_loss_dev, st.dp = topo_w2_device(pairs, cnt, vals, entries, maps, lamda=self.lamda, feat_d=1,
                                                      loss_q=2, want_grad=want_grad)
-        st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
+        self._dicece(st)
         main.wait_stream(side)
         if not torch.cuda.is_current_stream_capturing():  # (a captured graph owns its memory)
             for t in (st.topo_loss_dev, st.dp):
                 if t is not None:
                     t.record_stream(main)
+
+    def _dicece(self, st):
+        """DiceCE loss + backward. fused_pp (default): fused with the post-processing adjoint's row pass, the
+        topological loss's maps kept as d-masks for B (losses.dicece_pp_rows); else the [B, N, H, W] d-mask."""
+        B, N, H, W = st.masks.shape
+        if self.fused_pp:
+            maps = st.topo_dev[1] if st.topo_dev is not None else ()
+            st.loss3, st.pp_tmp, st.dkeep = dicece_pp_rows(st.masks, st.gt_u8.view(B, N, H, W), st.dpart, st.crop,
+                                                           maps=maps)
+            st.dmask = None
+        else:
+            st.loss3, st.dmask = dicece_forward_backward(st.masks, st.gt_u8.view(B, N, H, W), st.dpart)
 
     def _topo_host(self, st, backward):
         """-> topo loss (float); in backward mode also fills the device (eager) / pinned (graph) gradient.
@@ -196,8 +211,15 @@ class FusedTrainStep:
             if st.topo_dev is not None:
                 if self.w2 == "host" and st.pinned is not None:
                     st.dp.copy_(st.dp_pinned, non_blocking=True)
-                topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dmask, interp=self.interp)
-            dlow = postproc_backward(st.dmask.view(B * N, H, W), 256, st.crop, st.orig)
+                if self.fused_pp:
+                    topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dkeep, interp=self.interp, compact=True)
+                else:
+                    topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dmask, interp=self.interp)
+            if self.fused_pp:
+                dlow = pp_rows_finish(st.pp_tmp, st.crop, st.orig, dkeep=st.dkeep,
+                                      midx=st.topo_dev[2] if st.topo_dev is not None else None)
+            else:
+                dlow = postproc_backward(st.dmask.view(B * N, H, W), 256, st.crop, st.orig)
             self.model.mask_decoder.backward_impl(st.saved, dlow.view(B, N, 1, 256, 256))
         loss = st.loss_out
         loss[0:2] = st.loss3[0:2]

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 18
+#define OCTSAM_ABI_VERSION 19
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -342,6 +342,22 @@ int octsam_loss_finalize(const double* dice_map, int32_t M, const double* ce_par
 int octsam_postproc_bwd(const float* dout, int32_t M, int32_t S, int32_t out_h, int32_t out_w, const int32_t* col_ptr,
                         const int32_t* col_idx, const float* col_w, const int32_t* row_ptr, const int32_t* row_idx,
                         const float* row_w, float* tmp, float* dlowres, void* stream);
+/* The DiceCE backward fused with the post-processing adjoint's row pass (ABI 19; the d-mask round trip of
+ * octsam_dicece_bwd + octsam_postproc_bwd): one workgroup per (image, output row) forms d(DiceCE)/d mask for all N
+ * prompts of the row (octsam_dicece_bwd's arithmetic) and writes tmp[m] rows (octsam_postproc_bwd's row pass) for
+ * every map m = b * N + n with keep[m] < 0; keep[m] = k >= 0 writes the d-mask row to dkeep [K, H, W] instead (maps
+ * whose topological gradient is added later: octsam_topo_bwd_compact, then octsam_pp_bwd_rows_maps into tmp).
+ * ce_part double [B * H]; octsam_loss_finalize with nblk = B * H. keep may be NULL (every map). N <= 32.
+ * octsam_pp_bwd_cols: the column pass of octsam_postproc_bwd on its own (tmp fp32 [M, out_h, S] -> dlowres). */
+int octsam_dicece_pp_rows(const float* masks, const uint8_t* gt, const float* coef, int32_t B, int32_t N, int32_t H,
+                          int32_t W, float w_dice, float w_ce, int32_t S, const int32_t* col_ptr, const int32_t* col_idx,
+                          const float* col_w, const int32_t* keep, float* dkeep, float* tmp, double* ce_part,
+                          void* stream);
+int octsam_pp_bwd_rows_maps(const float* dout_k, const int32_t* map_idx, int32_t K, int32_t S, int32_t out_h,
+                            int32_t out_w, const int32_t* col_ptr, const int32_t* col_idx, const float* col_w, float* tmp,
+                            void* stream);
+int octsam_pp_bwd_cols(const float* tmp, int32_t M, int32_t S, int32_t out_h, const int32_t* row_ptr,
+                       const int32_t* row_idx, const float* row_w, float* dlowres, void* stream);
 
 /* ---------------------------------------------------------------- topological loss (dense parts)
  * ref:octsam/models/topological_loss.py:33-46: pred = interp(f(masks[map_idx[k]]), out_h x out_w,
@@ -353,6 +369,10 @@ int octsam_topo_down(const float* masks, const uint8_t* gt, const int32_t* map_i
                      void* stream);
 int octsam_topo_bwd(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h, int32_t in_w, int32_t out_h,
                     int32_t out_w, int32_t apply_sigmoid, const float* dpred, float scale, float* dmask, void* stream);
+/* octsam_topo_bwd into compact storage (ABI 19): dmask_k [K, in_h, in_w] holds the K maps themselves. */
+int octsam_topo_bwd_compact(const float* masks, const int32_t* map_idx, int32_t K, int32_t in_h, int32_t in_w,
+                            int32_t out_h, int32_t out_w, int32_t apply_sigmoid, const float* dpred, float scale,
+                            float* dmask_k, void* stream);
 /* HOST function (all pointers host): exact q-Wasserstein transport cost (before the 1/q power)
  * between diagrams d1 [n,2] and d2 [m,2] with L-inf ground metric and diagonal augmentation
  * (torch_topological WassersteinDistance -> POT ot.emd2, ref:octsam/models/topological_loss.py:78-82),
