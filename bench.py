@@ -34,18 +34,20 @@ MI355X_HBM_GBS = 8000.0  # HBM3E peak, same guide
 _E = 4096 * 256 * 2
 DEC_FWD_BYTES_PER_PROMPT = 12 * _E
 DEC_BWD_BYTES_PER_PROMPT = 24 * _E
-# HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes (FETCH_SIZE x2 for
-# gfx950's half-counted wide reads + WRITE_SIZE; scripts/gpu_round.sh -> scripts/pmc_traffic.py), same bench
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_gemm8.json")
+# HBM bytes per launch of the dominant kernel family from the committed rocprofv3 PMC passes (FETCH_SIZE x2 for
+# gfx950's half-counted wide reads + WRITE_SIZE; scripts/gpu_traffic.sh -> scripts/pmc_traffic.py), same bench.
+# The family files (round 4) average the same launch set as roofline.compulsory_bytes_per_launch (octsam_gemm path 2:
+# gemm8_kernel, gemm8p_kernel, gemm4w_kernel); the older gemm8-only files are used only where no family file exists.
+FAMILY_KERNELS = "gemm8_kernel,gemm8p_kernel,gemm4w_kernel"
 
 
 def traffic_json(args) -> str:
-    """PMC traffic file of the dominant GEMM for this workload (collected on the same bench flags by
-    scripts/gpu_round.sh): vit-base bf16 -> traffic_gemm8.json, otherwise traffic_gemm8_<model>_<dtype>.json."""
+    """PMC traffic file of the dominant GEMM family for this workload: vit-base bf16 -> traffic_gemm_family.json,
+    otherwise traffic_gemm_family_<model>_<dtype>.json; falls back to the gemm8-only traffic_gemm8*.json."""
     short = args.model.rsplit("/", 1)[-1]
-    if short == "sam-vit-base" and args.dtype == "bf16":
-        return TRAFFIC_JSON
-    return os.path.join(ROOT, "profiles", f"traffic_gemm8_{short}_{args.dtype}.json")
+    tag = "" if (short == "sam-vit-base" and args.dtype == "bf16") else f"_{short}_{args.dtype}"
+    fam = os.path.join(ROOT, "profiles", f"traffic_gemm_family{tag}.json")
+    return fam if os.path.exists(fam) else os.path.join(ROOT, "profiles", f"traffic_gemm8{tag}.json")
 
 
 def log(msg):
@@ -745,12 +747,18 @@ def main():
             achieved = flops / (ms * 1e-3) / 1e12
             traffic = None
             tj = traffic_json(args)
+            traffic_set = None
             if os.path.exists(tj):
-                traffic = round(json.load(open(tj))["hbm_bytes_per_launch"])
+                tjd = json.load(open(tj))
+                traffic = round(tjd["hbm_bytes_per_launch"])
+                traffic_set = ("the same launch set as compulsory_bytes_per_launch (" + tjd["kernel"] + ")"
+                               if "," in tjd["kernel"] else
+                               f"{tjd['kernel']} launches only (compulsory_bytes_per_launch averages the whole family)")
             roof = {"bound": "mfma", "kernel": dominant_name(args),
                     "achieved": round(achieved, 2), "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / MI355X_BF16_DENSE_TFLOPS, 4), "traffic": traffic,
                     "traffic_source": os.path.relpath(tj, ROOT) if traffic is not None else None,
+                    "traffic_launch_set": traffic_set,
                     "compulsory_bytes_per_launch": round(timer.bytes / n),
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}

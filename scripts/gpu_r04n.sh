@@ -1,0 +1,7 @@
+#!/bin/bash
+set -u
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-r04n}; mkdir -p $O; cd $R
+STEP_VARIANTS=default,n192 timeout -k 10 400 python -u scripts/step_ab3.py > $O/step_ab.log 2>&1 || { tail -10 $O/step_ab.log; exit 1; }
+tail -1 $O/step_ab.log
+STEP_PIPELINE=0 STEP_VARIANTS=default,n192 timeout -k 10 400 python -u scripts/step_ab3.py > $O/step_ab_seq.log 2>&1 || { tail -10 $O/step_ab_seq.log; exit 1; }
+tail -1 $O/step_ab_seq.log

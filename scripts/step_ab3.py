@@ -5,7 +5,8 @@ GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence for
 the DiceCE backward too, ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
 the mask-head backward, g4res_off = the decoder's [K | Q' | V] projection on the persistent 8-phase GEMM in plain tile
 order, octsam_gemm fast path 1 | 1024 | 2048, while capturing; attn_v2 = the global attention with whole rel_h
-tables, two workgroups per CU; pp_unfused = the DiceCE backward and the post-processing row pass as two kernels with
+tables, two workgroups per CU; n192 = octsam_gemm fast path 24 (256x192 tiles where they fill the waves better, the
+8-phase kernels otherwise); pp_unfused = the DiceCE backward and the post-processing row pass as two kernels with
 the [B, N, H, W] d-mask between them). Interleaved rounds, median of 5 rounds x 20 steps.
 Diagnostic only."""
 import json
@@ -33,8 +34,9 @@ def main():
     # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
     VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
                 "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
-                "g4res_off": ({}, {}), "attn_v2": ({}, {}), "pp_unfused": ({"fused_pp": False}, {})}
-    FAST = {"g4res_off": 1 | 1024 | 2048}
+                "g4res_off": ({}, {}), "attn_v2": ({}, {}), "pp_unfused": ({"fused_pp": False}, {}),
+                "n192": ({}, {})}
+    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
