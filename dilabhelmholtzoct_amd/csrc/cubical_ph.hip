@@ -270,6 +270,37 @@ __device__ __forceinline__ int block_scan_incl(int x, int* wtot, int tid) {
 __device__ __forceinline__ int vert_pos(const Map& m, int vid) { return 2 * (vid % (m.W + 1)) + m.W2 * 2 * (vid / (m.W + 1)); }
 __device__ __forceinline__ int pos_vert(const Map& m, int pos) { return (pos % m.W2) / 2 + (m.W + 1) * ((pos / m.W2) / 2); }
 
+// one pending edge J of a chunk: its current roots from the flattened root registers (lanes 2J', 2J' + 1, J' = J
+// mod 32, of A for J < 32, of B above), the merge (younger root -> older root) relabelled in every lane of the
+// registers still holding unresolved edges (BOTH: A and B; else the one J is in), young | old << 16 written into
+// lane J of rec. J is a compile-time constant so every lane select is an immediate (v_writelane's too: lanes
+// 0-63 are inline constants, which leave its scalar data operand the one constant-bus read).
+template <int DIM, bool BOTH, int J>
+__device__ __forceinline__ void uf_edge(int& A, int& B, int& rec) {
+  constexpr int L = 2 * (J & 31);
+  int& R = J < 32 ? A : B;
+  const int sa = __builtin_amdgcn_readlane(R, L);
+  const int sc = __builtin_amdgcn_readlane(R, L + 1);
+  const int young = DIM == 0 ? max(sa, sc) : min(sa, sc);
+  const int old = DIM == 0 ? min(sa, sc) : max(sa, sc);
+  R = R == young ? old : R;
+  if (BOTH) B = B == young ? old : B;
+  int pk;
+  asm("s_pack_ll_b32_b16 %0, %1, %2" : "=s"(pk) : "s"(young), "s"(old));
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rec) : "s"(pk), "i"(J));
+}
+template <int DIM, bool BOTH, int J0>
+__device__ __forceinline__ void uf_edges8(int& A, int& B, int& rec) {
+  uf_edge<DIM, BOTH, J0 + 0>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 1>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 2>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 3>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 4>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 5>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 6>(A, B, rec);
+  uf_edge<DIM, BOTH, J0 + 7>(A, B, rec);
+}
+
 // Elder-rule union-find over filtration RANKS (node id order == filtration order, so "younger" is an
 // integer comparison), 64 edges per chunk: lanes find their edge's roots against the chunk-start state in
 // parallel, then a wave-uniform loop resolves the 64 edges in order (readlane the two roots, min/max,
@@ -283,7 +314,12 @@ __device__ void uf_wave(Smem& s, const Map& m, int ne, int npix) {
   const uint32_t* epos = (const uint32_t*)s.keys;
   uint32_t* log = (uint32_t*)s.keys + NP2 + DIM * (m.H + 1) * (m.W + 1);  // H0 log <= nv-1, H1 log <= npix
   u16* par = s.u.uf.par[DIM];
+  // pending-edge scratch (3 x 64 ints per wave) past the union-find arrays (free until the pair records)
+  int* cs = (int*)((char*)&s.u + sizeof(s.u.uf)) + DIM * 192;
   int cnt = 0;
+#ifdef PH_PROFILE
+  unsigned long long t_find = 0, t_res = 0, t0 = __builtin_readcyclecounter();
+#endif
   for (int base = 0; base < ne; base += 64) {
     const int idx = DIM == 0 ? base + lane : ne - 1 - (base + lane);
     const bool valid = base + lane < ne;
@@ -309,35 +345,81 @@ __device__ void uf_wave(Smem& s, const Map& m, int ne, int npix) {
         ru = a < 0 ? npix : s.u.uf.prank[a];
         rv = c < 0 ? npix : s.u.uf.prank[c];
       }
-      ru = uf_find(par, ru);
-      rv = uf_find(par, rv);
+      // both finds walk together (two independent LDS latency chains per step); path halving on the way, then
+      // the edge's own nodes point straight at their roots
+      const int nu = ru, nv = rv;
+      int pu = par[ru], pv = par[rv];
+      while (pu != ru || pv != rv) {
+        const int gu = par[pu], gv = par[pv];
+        if (pu != ru) par[ru] = (u16)gu;
+        if (pv != rv) par[rv] = (u16)gv;
+        ru = gu;
+        rv = gv;
+        pu = par[ru];
+        pv = par[rv];
+      }
+      if (nu != ru) par[nu] = (u16)ru;
+      if (nv != rv) par[nv] = (u16)rv;
     }
-    int my_young = -1, my_old = 0;
-    // branch-free: an edge whose roots already agree relabels nothing (young == old) and is not recorded;
-    // the invalid tail lanes hold ru == rv == 0 (walking only the lanes whose roots differ at the chunk start,
-    // an s_ff1 loop with a lane-indexed readlane, measured slower: 427 -> 493 us per launch)
-#pragma unroll 8
-    for (int j = 0; j < 64; ++j) {
-      const int sa = __builtin_amdgcn_readlane(ru, j);
-      const int sc = __builtin_amdgcn_readlane(rv, j);
-      const int young = DIM == 0 ? max(sa, sc) : min(sa, sc);
-      const int old = DIM == 0 ? min(sa, sc) : max(sa, sc);
-      ru = ru == young ? old : ru;
-      rv = rv == young ? old : rv;
-      const bool rec = lane == j && sa != sc;
-      my_young = rec ? young : my_young;
-      my_old = rec ? old : my_old;
+    // Only the edges whose roots differ at the chunk start can merge: relabelling maps both roots of an edge through
+    // the same function, so roots that agree keep agreeing (and such an edge is not recorded). Those edges are
+    // compacted in edge order through this wave's LDS scratch, their roots flattened edge-major (edge j's at lanes
+    // 2j, 2j + 1 of A for j < 32, of B above; zeros past them are no-op pairs), and the wave-uniform loop resolves
+    // only them, 8 at a time. Edges past the first 32 relabel B alone. (Per pending edge: 2 readlanes, scalar
+    // min/max, 2-4 VALU relabel, one writelane of young | old << 16 into the edge's lane; a compare-and-select
+    // record over both roots in every lane, and an s_ff1 walk over the pending mask, measured slower.)
+#ifdef PH_PROFILE
+    { const unsigned long long t1 = __builtin_readcyclecounter(); t_find += t1 - t0; t0 = t1; }
+#endif
+    const bool pend = ru != rv;  // (invalid tail lanes hold ru == rv == 0)
+    const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
+    const int np = __builtin_popcountll(pm);
+    if (pend) {
+      const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0));
+      cs[2 * p] = ru;
+      cs[2 * p + 1] = rv;
+      cs[128 + p] = idx;
     }
-    const bool merged = my_young >= 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int A = lane < 2 * np ? cs[lane] : 0;
+    int B = lane + 64 < 2 * np ? cs[64 + lane] : 0;
+    const int cidx = lane < np ? cs[128 + lane] : 0;
+    int rec = 0;
+    // edges past np hold zero roots (no-op merges); groups of 8 up to np, B relabelled only while it holds edges
+    if (np <= 32) {
+      if (np > 0) uf_edges8<DIM, false, 0>(A, B, rec);
+      if (np > 8) uf_edges8<DIM, false, 8>(A, B, rec);
+      if (np > 16) uf_edges8<DIM, false, 16>(A, B, rec);
+      if (np > 24) uf_edges8<DIM, false, 24>(A, B, rec);
+    } else {
+      uf_edges8<DIM, true, 0>(A, B, rec);
+      uf_edges8<DIM, true, 8>(A, B, rec);
+      uf_edges8<DIM, true, 16>(A, B, rec);
+      uf_edges8<DIM, true, 24>(A, B, rec);
+      uf_edges8<DIM, false, 32>(A, B, rec);
+      if (np > 40) uf_edges8<DIM, false, 40>(A, B, rec);
+      if (np > 48) uf_edges8<DIM, false, 48>(A, B, rec);
+      if (np > 56) uf_edges8<DIM, false, 56>(A, B, rec);
+    }
+    const int my_young = rec & 0xffff, my_old = rec >> 16;
+    const bool merged = my_young != my_old;  // (lanes past np hold rec == 0)
     if (merged) par[my_young] = (u16)my_old;
     const uint64_t mask = __builtin_amdgcn_ballot_w64(merged);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-    if (merged) log[cnt + below] = ((uint32_t)my_young << 13) | (uint32_t)idx;
+    if (merged) log[cnt + below] = ((uint32_t)my_young << 13) | (uint32_t)cidx;
     cnt += __builtin_popcountll(mask);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#ifdef PH_PROFILE
+    { const unsigned long long t1 = __builtin_readcyclecounter(); t_res += t1 - t0; t0 = t1; }
+#endif
   }
   if (lane == 0) s.nlog[DIM] = cnt;
+#ifdef PH_PROFILE
+  if (lane == 0 && blockIdx.x == 0) { g_ph_stamp[16 + 2 * DIM] = t_find; g_ph_stamp[17 + 2 * DIM] = t_res; }
+#endif
 }
 
 __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restrict__ maps, int H, int W, int max_pairs,

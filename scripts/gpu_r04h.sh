@@ -7,6 +7,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -1 $O/pytest_ph.log
 timeout -k 10 60 ./scripts/micro/ph_timing_probe > $O/ph_timing.log 2>&1 || { tail -5 $O/ph_timing.log; exit 1; }
 cat $O/ph_timing.log
+if [ -x ./scripts/micro/uf_resolve_probe ]; then timeout -k 10 60 ./scripts/micro/uf_resolve_probe > $O/uf_resolve_probe.log 2>&1 || exit 1; cat $O/uf_resolve_probe.log; fi
 timeout -k 10 400 python -u -m pytest -x -v --timeout 280 --timeout-method thread tests/test_gpu_losses.py tests/test_gpu_graph_step.py tests/test_gpu_pipeline.py > $O/pytest_b.log 2>&1 || { tail -30 $O/pytest_b.log; exit 1; }
 tail -1 $O/pytest_b.log
 cd /tmp && export TMPDIR=/tmp

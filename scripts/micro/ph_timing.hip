@@ -27,6 +27,7 @@ int main() {
     unsigned long long cur[] = {st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
     for (int k = 0; k < 7; ++k) printf("  %-10s %10llu cycles\n", names[k], cur[k] - prev[k]);
     printf("  total      %10llu cycles\n", st[7] - st[0]);
+    for (int d = 0; d < 2; ++d) printf("  H%d find %llu resolve %llu cycles\n", d, st[16 + 2 * d], st[17 + 2 * d]);
   }
   return 0;
 }
