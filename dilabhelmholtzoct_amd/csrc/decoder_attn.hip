@@ -424,6 +424,173 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
   for (int i = 0; i < 4; ++i) w[(4 * g + i) * 16 + c] = dqs[i];
 }
 
+// Backward of the shared-K/V form (kv_rep > 1: layer 0's keys are the image embedding, shared by the image's kv_rep
+// prompts, hf modeling_sam.py:499-501 repeat_interleave) with the prompt sum of dK / dV fused in: a workgroup =
+// (image, 64-key chunk), wave = head pair; the chunk's K / V slices are staged in LDS once and the workgroup walks the
+// image's prompts in order, accumulating dK^T / dV^T of its 64 keys in fp32 registers over the prompts (the per-prompt
+// arithmetic of t2i_bwd_kernel), and stores them once per image -- the per-prompt [P*L, 2*CI] gradients and their
+// prompt-sum pass never touch HBM. The next prompt's token operands load while the current prompt computes; its row
+// statistics (log2 lse, dO . O) come precomputed from t2i_rowstats_kernel. dQ partials as in t2i_bwd_kernel.
+namespace t2s {
+constexpr int SCH = 64;                          // keys per workgroup chunk (2 steps)
+constexpr int WAVE_LDS = 2 * t2::STEP_BYTES;     // 8 KiB per wave
+constexpr int SMEM = 4 * WAVE_LDS;
+}  // namespace t2s
+
+// st fp32 [P][8][Tq][2] = (lse * log2(e), dO . O) per (prompt, head, token) (the bwd kernels' row constants)
+__global__ void t2i_rowstats_kernel(const float* __restrict__ dout, const bf16* __restrict__ out,
+                                    const float* __restrict__ lse, int Tq, float* __restrict__ st) {
+  const int p = blockIdx.x, t = threadIdx.x;
+  if (t >= 8 * Tq) return;
+  const int h = t / Tq, qi = t - h * Tq;
+  const float* a = dout + ((long long)p * Tq + qi) * 128 + h * 16;
+  const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
+  float s = 0.0f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+  float* w = st + (((long long)p * 8 + h) * Tq + qi) * 2;
+  w[0] = lse[((long long)p * 8 + h) * Tq + qi] * t2::L2E;
+  w[1] = s;
+}
+
+__global__ __launch_bounds__(256) void t2i_bwd_sum_kernel(const float* __restrict__ q, const bf16* __restrict__ k,
+                                                          const bf16* __restrict__ v, long long ldkv, int kv_rep,
+                                                          int Tq, int L, int nchunk, const float* __restrict__ dout,
+                                                          const float* __restrict__ st, bf16* __restrict__ dk,
+                                                          bf16* __restrict__ dv, long long lddkv,
+                                                          float* __restrict__ part) {
+  using namespace t2;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int img = blockIdx.x / nchunk, chunk = blockIdx.x - img * nchunk;
+  const int key0 = chunk * t2s::SCH;
+  char* ring = tsm + hp * t2s::WAVE_LDS;
+  const long long kvb = (long long)img * L;
+  const bf16* kb = k + kvb * ldkv + hp * 32;
+  const bf16* vb = v + kvb * ldkv + hp * 32;
+  load_step(kb, ldkv, vb, ldkv, key0, ring, lane);
+  load_step(kb, ldkv, vb, ldkv, key0 + STEP, ring + STEP_BYTES, lane);
+  // token operands of one prompt, loaded raw (fp32) so the next prompt's loads overlap this prompt's products
+  struct Raw {
+    float qv[8], dv8[8], dT[2][4], qT[2][4], cs[2], rs[4][2];
+  };
+  auto load_raw = [&](int p, Raw& r) {
+    const int qi = c & 7;
+    const bool on = (g >> 1) == (c >> 3) && qi < Tq;
+    const float* qs = q + ((long long)p * Tq + (on ? qi : 0)) * 128 + hp * 32 + 8 * g;
+    const float* ds = dout + ((long long)p * Tq + (on ? qi : 0)) * 128 + hp * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r.qv[j] = on ? qs[j] : 0.0f;
+      r.dv8[j] = on ? ds[j] : 0.0f;
+    }
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 4 * g + j, qj = n & 7;
+        const bool o2 = (n >> 3) == hl && qj < Tq;
+        const long long e = ((long long)p * Tq + (o2 ? qj : 0)) * 128 + (2 * hp + hl) * 16 + c;
+        r.dT[hl][j] = o2 ? dout[e] : 0.0f;
+        r.qT[hl][j] = o2 ? q[e] : 0.0f;
+      }
+    auto cst = [&](int n, float* o) {
+      const int qn = n & 7, h = 2 * hp + (n >> 3);
+      if (qn >= Tq) {
+        o[0] = INFINITY;
+        o[1] = 0.0f;
+        return;
+      }
+      const float* w = st + (((long long)p * 8 + h) * Tq + qn) * 2;
+      o[0] = w[0];
+      o[1] = w[1];
+    };
+    cst(c, r.cs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cst(4 * g + i, r.rs[i]);
+  };
+  f32x4 adk[2][2][2], adv[2][2][2];  // [step][16-key half][head of the pair]
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) adk[s2][t][hl] = adv[s2][t][hl] = (f32x4)0.0f;
+  Raw cur, nxt;
+  load_raw(img * kv_rep, cur);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chunk's K / V slices (and the first prompt's operands)
+  __builtin_amdgcn_wave_barrier();
+  for (int pi = 0; pi < kv_rep; ++pi) {
+    const int p = img * kv_rep + pi;
+    if (pi + 1 < kv_rep) load_raw(p + 1, nxt);
+    bf16x8 qhi, qlo, dop;
+    const float qs = 0.25f * L2E;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v8 = cur.qv[j] * qs;
+      qhi[j] = (bf16)v8;
+      qlo[j] = (bf16)(v8 - (float)qhi[j]);
+      dop[j] = (bf16)cur.dv8[j];
+    }
+    s16x4 adO[2], aQ[2];
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        adO[hl][j] = __builtin_bit_cast(short, (bf16)cur.dT[hl][j]);
+        aQ[hl][j] = __builtin_bit_cast(short, (bf16)(cur.qT[hl][j] * 0.25f));
+      }
+    const float lc2 = cur.cs[0], dc = cur.cs[1];
+    f32x4 dq0 = (f32x4)0.0f, dq1 = (f32x4)0.0f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const char* slot = ring + s2 * STEP_BYTES;
+      const char* vimg = slot + 2048;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8 kf = row_op(slot, t, false, lane), vf = row_op(vimg, t, true, lane);
+        f32x4 sT = mfma32(kf, qhi, (f32x4)0.0f);
+        sT = mfma32(kf, qlo, sT);
+        const f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);
+        f32x4 sS = mfma32(qhi, kf, (f32x4)0.0f);
+        sS = mfma32(qlo, kf, sS);
+        const f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+        f32x4 dsT, pS, dsS;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dsT[i] = __builtin_amdgcn_exp2f(sT[i] - lc2) * (dpT[i] - dc);
+          pS[i] = __builtin_amdgcn_exp2f(sS[i] - cur.rs[i][0]);
+          dsS[i] = pS[i] * (dpS[i] - cur.rs[i][1]);
+        }
+        const s16x4 pSb = pack4(pS), dsSb = pack4(dsS), dsTb = pack4(dsT);
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          adv[s2][t][hl] = mfma16(adO[hl], pSb, adv[s2][t][hl]);
+          adk[s2][t][hl] = mfma16(aQ[hl], dsSb, adk[s2][t][hl]);
+        }
+        dq0 = mfma16(dsTb, tr_op(slot, t, 0, false, lane), dq0);
+        dq1 = mfma16(dsTb, tr_op(slot, t, 1, false, lane), dq1);
+      }
+    }
+    float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * 256;
+    const f32x4 dqs = g < 2 ? dq0 : dq1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[(4 * g + i) * 16 + c] = dqs[i];
+    if (pi + 1 < kv_rep) cur = nxt;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const long long row = (kvb + key0 + s2 * STEP + 16 * t + c) * lddkv + 32 * hp + 4 * g;
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        *(s16x4*)(dv + row + 16 * hl) = pack4(adv[s2][t][hl]);
+        *(s16x4*)(dk + row + 16 * hl) = pack4(adk[s2][t][hl]);
+      }
+    }
+}
+
 // dq bf16 [P,Tq,128] = 0.25 * sum over chunks (in order) of the dQ partials
 __global__ void t2i_dq_kernel(const float* __restrict__ part, int nchunk, int Tq, bf16* __restrict__ dq) {
   const int p = blockIdx.x, t = threadIdx.x;
@@ -671,6 +838,40 @@ extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, 
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
   hipLaunchKernelGGL(t2i_dq_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)dq);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
+  return 0;
+}
+
+// the shared-K/V backward with the prompt sum fused in (t2i_bwd_sum_kernel): dk / dv are the IMAGE rows
+// [(P / kv_rep) * L, lddkv]; workspace: octsam_dec_t2i_bwd_sum_workspace(P, Tq, L) floats
+extern "C" int64_t octsam_dec_t2i_bwd_sum_workspace(int32_t P, int32_t Tq, int32_t L) {
+  return (int64_t)P * (L / t2s::SCH) * 4 * 256 + (int64_t)P * 8 * Tq * 2;
+}
+
+extern "C" int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
+                                      int32_t P, int32_t Tq, int32_t L, const void* out, const float* dout,
+                                      const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace,
+                                      void* stream) {
+  OCTSAM_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv && workspace && P > 0 && Tq > 0 &&
+                       Tq <= MAXT && L > 0 && L % t2s::SCH == 0 && kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 &&
+                       lddkv % 4 == 0 && (uintptr_t)k % 16 == 0 && (uintptr_t)v % 16 == 0 &&
+                       (uintptr_t)dk % 8 == 0 && (uintptr_t)dv % 8 == 0,
+                   "octsam_dec_t2i_bwd_sum: bad args");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)t2i_bwd_sum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, t2s::SMEM);
+    attr = true;
+  }
+  const int nch = L / t2s::SCH, nimg = P / kv_rep;
+  float* part = workspace;
+  float* st = workspace + (int64_t)P * nch * 4 * 256;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(t2i_rowstats_kernel, dim3(P), dim3(64), 0, s, dout, (const bf16*)out, lse, Tq, st);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd_sum");
+  hipLaunchKernelGGL(t2i_bwd_sum_kernel, dim3(nimg * nch), dim3(256), t2s::SMEM, s, q, (const bf16*)k, (const bf16*)v,
+                     ldkv, kv_rep, Tq, L, nch, dout, st, (bf16*)dk, (bf16*)dv, lddkv, part);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd_sum");
+  hipLaunchKernelGGL(t2i_dq_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, part, nch, Tq, (bf16*)dq);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd_sum");
   return 0;
 }
 

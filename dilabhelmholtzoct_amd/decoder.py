@@ -280,6 +280,9 @@ class MaskDecoder(nn.Module):
     # token-side weight + bias gradients through octsam_wgrad_tok (False: split-K tile GEMM + reduction + column-sum
     # kernel + reduction; A/B, scripts/step_ab3.py)
     tok_wgrad = True
+    # the first block's token->image backward with the prompt sum of its shared K / V gradients fused in
+    # (octsam_dec_t2i_bwd_sum; False: per-prompt gradients + octsam_group_sum; A/B, scripts/step_ab3.py)
+    t2i_sum = True
     # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
     fused_ln_bwd = True
@@ -725,7 +728,13 @@ class MaskDecoder(nn.Module):
             dto = torch.empty(R, CI, device=dev, dtype=f32)
             self._lin_bwd(ds_b, ls.t2i_o_b, t2i + "out_proj.weight", t2i + "out_proj.bias", R, dx_out=dto)
             dQ = torch.empty(R, CI, device=dev, dtype=b16)
-            if li == 0:
+            dKV_img = None
+            if li == 0 and self.t2i_sum and ls.kv_rep > 1 and L % 64 == 0:
+                # K / V shared by the image's prompts: their gradients summed over the prompts inside the kernel
+                dKV_img = torch.empty(B * L, 2 * CI, device=dev, dtype=b16)
+                K.t2i_bwd_sum(ls.t2i_Q, KQV, KQV[:, 2 * CI:], 3 * CI, ls.kv_rep, P, T, L, ls.t2i_o_b, dto, ls.t2i_lse,
+                              dQ, dKV_img, dKV_img[:, CI:], 2 * CI)
+            elif li == 0:
                 dKV0 = torch.empty(RL, 2 * CI, device=dev, dtype=b16)
                 K.t2i_bwd(ls.t2i_Q, KQV, KQV[:, 2 * CI:], 3 * CI, ls.kv_rep, P, T, L, ls.t2i_o_b, dto, ls.t2i_lse, dQ,
                           dKV0, dKV0[:, CI:], 2 * CI)
@@ -738,17 +747,21 @@ class MaskDecoder(nn.Module):
             if li == 0:
                 # per-image tensors: sum the per-prompt gradients over the image's prompts first
                 Mi = B * L
-                dK_img = torch.empty(Mi, CI, device=dev, dtype=b16)
+                ldkv = CI
+                if dKV_img is not None:
+                    dK_img, dV_img, ldkv = dKV_img, dKV_img[:, CI:], 2 * CI
+                else:
+                    dK_img = torch.empty(Mi, CI, device=dev, dtype=b16)
+                    dV_img = torch.empty(Mi, CI, device=dev, dtype=b16)
+                    K.group_sum(dKV0, dK_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
+                    K.group_sum(dKV0[:, CI:], dV_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 dQ_img = torch.empty(Mi, CI, device=dev, dtype=b16)
-                dV_img = torch.empty(Mi, CI, device=dev, dtype=b16)
-                K.group_sum(dKV0, dK_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
-                K.group_sum(dKV0[:, CI:], dV_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                 K.group_sum(dQp, dQ_img, ld_in=CI, cols=CI, groups=B, nper=N, rows_per=L)
-                self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), x_add=s.pe_b, x_add_rows=L,
+                self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), ldy=ldkv, x_add=s.pe_b, x_add_rows=L,
                          db=self.G(t2i + "k_proj.bias"))
                 self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L,
                          db=self.G(i2t + "q_proj.bias"))
-                self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"), db=self.G(t2i + "v_proj.bias"))
+                self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"), ldy=ldkv, db=self.G(t2i + "v_proj.bias"))
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
                 self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)

@@ -326,6 +326,16 @@ def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
               ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
 
 
+def t2i_bwd_sum(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
+    """t2i_bwd for K / V shared by kv_rep prompts per image with the prompt sum fused in: dk, dv are the image rows
+    [(P / kv_rep) * L, lddkv] (octsam_dec_t2i_bwd_sum)."""
+    _require_cuda(q, k, v, out, dout, lse, dq, dk, dv)
+    n = _lib.load().octsam_dec_t2i_bwd_sum_workspace(P, Tq, L)
+    ws = torch.empty(n, device=q.device, dtype=torch.float32)
+    _lib.call("octsam_dec_t2i_bwd_sum", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(dout), ptr(lse),
+              ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
+
+
 def i2t_fwd(q, ldq, q_rep, k, v, P, Tk, L, out, ldo):
     _lib.call("octsam_dec_i2t_fwd", ptr(q), ldq, q_rep, ptr(k), ptr(v), P, Tk, L, ptr(out), ldo)
 

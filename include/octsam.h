@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 19
+#define OCTSAM_ABI_VERSION 20
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -278,6 +278,14 @@ int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void* v, int64_
 int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P, int32_t Tq,
                        int32_t L, const void* out, const float* dout, const float* lse, void* dq, void* dk, void* dv,
                        int64_t lddkv, float* workspace, void* stream);
+/* octsam_dec_t2i_bwd for shared K / V (kv_rep prompts per image, the first two-way block) with the prompt sum fused
+ * in: dk / dv are the IMAGE rows [(P / kv_rep) * L, lddkv] (bf16) = sum over the image's prompts of the per-prompt
+ * gradients, accumulated in fp32 (replaces octsam_dec_t2i_bwd's per-prompt [P * L] rows + octsam_group_sum).
+ * L % 64 == 0; fp32 workspace of octsam_dec_t2i_bwd_sum_workspace(P, Tq, L) elements (ABI 20). */
+int64_t octsam_dec_t2i_bwd_sum_workspace(int32_t P, int32_t Tq, int32_t L);
+int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                           int32_t Tq, int32_t L, const void* out, const float* dout, const float* lse, void* dq,
+                           void* dk, void* dv, int64_t lddkv, float* workspace, void* stream);
 int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
                        int32_t L, void* out, int64_t ldo, void* stream);
 int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L);

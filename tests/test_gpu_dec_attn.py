@@ -64,6 +64,46 @@ def test_t2i_fwd_bwd(cuda, P, kv_rep, T, ld):
     assert _rel(dv, vr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("P,kv_rep,T,ld", [(6, 3, 7, 384), (21, 21, 7, 384), (8, 2, 5, 256), (4, 4, 1, 384)])
+def test_t2i_bwd_sum(cuda, P, kv_rep, T, ld):
+    """The shared-K/V backward with the prompt sum fused in (octsam_dec_t2i_bwd_sum: image-row dK / dV summed over
+    the image's prompts in fp32) vs torch fp32 autograd, vs the per-prompt kernel summed afterwards (same arithmetic,
+    one bf16 rounding instead of kv_rep + 1), and dq identical in value to the per-prompt kernel's up to the chunk
+    partition of its fp32 sum; bitwise repeatable."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(P * 13 + kv_rep + T)
+    B = P // kv_rep
+    buf = (torch.randn(B * L, ld, generator=g) * 1.5).to(cuda, torch.bfloat16)
+    vcol = ld - CI
+    q = (torch.randn(P, T, CI, generator=g) * 2).to(cuda)
+    out = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(P, H, T, device=cuda)
+    kernels.t2i_fwd(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, lse)
+    qr = q.clone().requires_grad_()
+    kr = buf[:, :CI].float().reshape(B, L, CI).requires_grad_()
+    vr = buf[:, vcol:].float().reshape(B, L, CI).requires_grad_()
+    oref, _ = _t2i_ref(qr, kr, vr, kv_rep)
+    dout = torch.randn(P, T, CI, generator=g).to(cuda)
+    oref.backward(dout)
+    dkv = torch.empty(B * L, 2 * CI, device=cuda, dtype=torch.bfloat16)
+    dq = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+    kernels.t2i_bwd_sum(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, dout, lse, dq, dkv, dkv[:, CI:], 2 * CI)
+    assert _rel(dq, qr.grad) < 2e-2
+    assert _rel(dkv[:, :CI].reshape(B, L, CI), kr.grad) < 2e-2
+    assert _rel(dkv[:, CI:].reshape(B, L, CI), vr.grad) < 2e-2
+    # the per-prompt kernel + the prompt sum
+    dkv1 = torch.empty(P * L, 2 * CI, device=cuda, dtype=torch.bfloat16)
+    dq1 = torch.empty(P, T, CI, device=cuda, dtype=torch.bfloat16)
+    kernels.t2i_bwd(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, dout, lse, dq1, dkv1, dkv1[:, CI:], 2 * CI)
+    s1 = dkv1.float().reshape(B, kv_rep, L, 2 * CI).sum(1).reshape(B * L, 2 * CI)
+    assert _rel(dkv, s1) < 1e-2
+    assert _rel(dq, dq1) < 1e-2
+    again = torch.empty_like(dkv)
+    dq2 = torch.empty_like(dq)
+    kernels.t2i_bwd_sum(q, buf, buf[:, vcol:], ld, kv_rep, P, T, L, out, dout, lse, dq2, again, again[:, CI:], 2 * CI)
+    assert torch.equal(again, dkv) and torch.equal(dq2, dq)
+
+
 def _i2t_ref(qimg, k, v, q_rep):
     """qimg [B, L, 128]; k, v [P, T, 128] -> out [P, L, 128]."""
     qq = qimg.repeat_interleave(q_rep, 0)
