@@ -490,12 +490,18 @@ def val_protocol(args, device):
 
     run(2000, 4, limit=64)
     hip = [dice()]
+    # the warm state the committed oracle values start from (tests/test_gpu_val_dice.py warm_fingerprint)
+    wsd = {n: t.detach().float().cpu() for n, t in model.mask_decoder.state_dict().items()}
+    fp = [round(sum(float(t.double().sum()) for t in wsd.values()), 6),
+          round(sum(float((t.double() ** 2).sum()) for t in wsd.values()), 6)]
+    del wsd
     run(2001, 4, evals=hip)
     ora = gold["oracle_dice"]
     diffs = [round(h - o, 5) for h, o in zip(hip, ora)]
     out = {"steps": gold["steps"], "hip": hip, "oracle": ora, "diff": diffs,
            "max_abs_diff": round(max(abs(d) for d in diffs), 5), "tolerance": 0.005,
            "within": bool(max(abs(d) for d in diffs) <= 0.005), "seconds": round(time.perf_counter() - t0, 1),
+           "warm_fingerprint": fp, "warm_state_matches_golden": fp == gold.get("warm_fingerprint"),
            "protocol": "tests/test_gpu_val_dice.py (warm start: 64 HIP steps; 4 epochs x 16 steps; 32 held-out scans)",
            "oracle_source": "tests/golden/valdice_oracle.json"}
     log(f"val protocol: {out}")

@@ -79,6 +79,14 @@ def warm_start(cuda, state):
     return weights, adam
 
 
+def warm_fingerprint(weights):
+    """(sum, sum of squares) of the warm decoder's weights in float64: identifies the HIP warm state the committed
+    oracle values (tests/golden/valdice_oracle.json) were made from -- bench.py compares it before quoting them."""
+    s = sum(float(t.double().sum()) for t in weights.values())
+    q = sum(float((t.double() ** 2).sum()) for t in weights.values())
+    return [round(s, 6), round(q, 6)]
+
+
 def load_torch_adam(opt, module, adam):
     """FusedTrainStep.optimizer_state() -> torch.optim.Adam state (parameters that never had a gradient, the IoU
     head, keep no state in torch)."""
@@ -156,6 +164,14 @@ def test_val_dice_parity(cuda):
     moved = float((w1 - w0).norm() / w0.norm())
     for kk, got, want in results:
         print(f"after {kk:3d} steps: val Dice HIP {got:.5f}  oracle {want:.5f}  diff {got - want:+.5f}")
+    fp = warm_fingerprint(weights)
+    print(f"warm-state fingerprint {fp}")
+    if os.environ.get("OCTSAM_VALDICE_OUT"):  # regenerating tests/golden/valdice_oracle.json (scripts/gpu_valdice_golden.sh)
+        import json
+        with open(os.environ["OCTSAM_VALDICE_OUT"], "w") as f:
+            json.dump({"steps": [kk for kk, _, _ in results], "oracle_dice": [round(w, 5) for _, _, w in results],
+                       "hip_dice_in_that_run": [round(g, 5) for _, g, _ in results], "warm_fingerprint": fp,
+                       "oracle_specificity": round(spec, 4), "oracle_moved": round(moved, 4)}, f, indent=1)
     print(f"oracle specificity at the end {spec:.4f}; oracle decoder moved {moved:.4f} (relative norm)")
     assert spec > 0.5, f"oracle specificity {spec:.4f}: the degenerate all-foreground regime"
     assert moved > 0.01, f"the oracle's decoder barely moved ({moved:.4g}): the compared epochs did not train"
