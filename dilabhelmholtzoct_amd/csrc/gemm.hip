@@ -25,6 +25,8 @@
 // Register-staged double buffer, one barrier per K-step; XCD-aware block remap so that the tiles
 // of one A row-panel run on one XCD (shared L2).
 #include "common.h"
+#include <cstdio>
+#include <cstdlib>
 #include "../../include/octsam.h"
 
 // 16-bit operand type of this build: bf16 (octsam_gemm) or IEEE half (built again with OCTSAM_GEMM_F16:
@@ -1232,7 +1234,8 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
                                               int lane, const float* lds_bias = nullptr) {
   constexpr bool CF32 = ((FE - 1) & 1) != 0, RES = ((FE - 1) & 2) != 0, RMAP = ((FE - 1) & 4) != 0;
   constexpr bool RREMAP = ((FE - 1) & 8) != 0;
-  constexpr int ES = CF32 ? 4 : 2;
+  constexpr bool RF32 = CF32 || ((FE - 1) & 16) != 0;  // bit 16: an fp32 residual under an e16 C
+  constexpr int ES = CF32 ? 4 : 2, RS = RF32 ? 4 : 2;
   const int q = lane >> 4;
   const int cofs = 16 * (q & 1) + 8 * (q >> 1);
   // descriptor origin / extent and each lane's row offsets (bytes)
@@ -1242,7 +1245,7 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
   const int c_bytes = RMAP ? p.c_rows * (int)p.ldc * ES : rows_left * (int)p.ldc * ES;
   // (a remapped residual has r_blk * ceil(M / (r_blk * r_rep)) stored rows: remap(m) < that for m < M)
   const int r_rows = RREMAP ? p.r_blk * ((p.M - 1) / (p.r_blk * p.r_rep) + 1) : 0;
-  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * ES : RREMAP ? r_rows * (int)p.ldr * ES : rows_left * (int)p.ldr * ES;
+  const int r_bytes = RMAP ? p.c_rows * (int)p.ldr * RS : RREMAP ? r_rows * (int)p.ldr * RS : rows_left * (int)p.ldr * RS;
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.C + c_origin * ES), (short)0, c_bytes, 0x00020000);
   uint32_t crow[NMI], rrow[NMI];
@@ -1253,11 +1256,11 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
       const int m = row0 + rl;
       const int om = m < p.M ? p.row_map[m] : -1;
       crow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldc * ES) : 0x80000000u;
-      rrow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldr * ES) : 0x80000000u;
+      rrow[j] = om >= 0 ? (uint32_t)(om * (int)p.ldr * RS) : 0x80000000u;
     } else {
       crow[j] = (uint32_t)(rl * (int)p.ldc * ES);
-      rrow[j] = RREMAP ? (uint32_t)((int)remap(row0 + rl, p.r_blk, p.r_rep) * (int)p.ldr * ES)
-                       : (uint32_t)(rl * (int)p.ldr * ES);
+      rrow[j] = RREMAP ? (uint32_t)((int)remap(row0 + rl, p.r_blk, p.r_rep) * (int)p.ldr * RS)
+                       : (uint32_t)(rl * (int)p.ldr * RS);
       if (RREMAP && row0 + rl >= p.M) rrow[j] = 0x80000000u;
     }
   }
@@ -1317,14 +1320,14 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
   float res[RES ? NMI : 1][2][8];
   if constexpr (RES) {
     const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.R + r_origin * ES), (short)0, r_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)((char*)p.R + r_origin * RS), (short)0, r_bytes, 0x00020000);
 #pragma unroll
     for (int j = 0; j < NMI; ++j)
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         // (columns past N read as zero: their offset is sent past the range like the stores')
-        const uint32_t o = colok[pr] ? rrow[j] + cl + (uint32_t)(32 * pr * ES) : 0x80000000u;
-        if constexpr (CF32) {
+        const uint32_t o = colok[pr] ? rrow[j] + (uint32_t)(cofs * RS) + (uint32_t)(32 * pr * RS) : 0x80000000u;
+        if constexpr (RF32) {
           const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
           const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o + 16, 0, 0));
 #pragma unroll
@@ -2003,6 +2006,7 @@ int launch_gemm4w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
 // the lean kinds of the encoder's GEMMs (QKV / MLP1: e16 C; projections: fp32 C + in-place fp32 residual, with
 // or without the window row map) on the two-workgroup kernel: fast path 0 (default) when g_gemm4w, K % 32 == 0
 static int g_gemm4w = 1;
+
 // the row-remapped broadcast-addend kind (11) on the two-workgroup kernel when N is not a multiple of 256: the
 // decoder's [K | Q' | V] projection of the per-prompt keys (M = P*4096, N = 384, K = 256) fills 256x128 tiles
 // exactly where 256x256 tiles waste a third; 320 -> 284 us, 270 with the rgroup_tm order (scripts/gemm_res_ab.py,
@@ -2069,9 +2073,17 @@ int launch_gemm8(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
       case 4: return launch_gemm8_fe<DBG, EPI, 4>(k, a, s);    // fp32 C + fp32 residual
       case 8: return launch_gemm8_fe<DBG, EPI, 8>(k, a, s);    // fp32 C + fp32 residual, row map
       case 11: return launch_gemm8_fe<DBG, EPI, 11>(k, a, s);  // e16 C + broadcast e16 residual
+      // e16 C + broadcast fp32 residual (one tile per workgroup: the persistent kernel, whose epilogue loads drain
+      // the next tile's prefetch, took 467.8 vs 198.3 us on the decoder's M = 688 128, N = 256, K = 128 call)
+      case 27: return launch_gemm8_fe<DBG, EPI, 27>(k, a, s);
       default: break;
     }
   }
+  if (DBG == 0 && std::getenv("OCTSAM_GEMM_TRACE"))  // diagnostics: which calls take the general epilogue
+    fprintf(stderr, "[gemm8 general epilogue] M=%d N=%d K=%d batch=%d act=%d fast_epi=%d c_f32=%d R=%d r_f32=%d r_blk=%d "
+                    "C_pre=%d row_map=%d ldc=%lld ldr=%lld C%%16=%d beta=%g\n", a->M, a->N, a->K, a->batch, a->act,
+            k.fast_epi, a->c_f32, a->R != nullptr, a->r_f32, a->r_blk, a->C_pre != nullptr, a->row_map != nullptr,
+            (long long)a->ldc, (long long)a->ldr, (int)((uintptr_t)a->C & 15), a->beta);
   return launch_gemm8_fe<DBG, EPI, 0>(k, a, s);
 }
 
@@ -2443,14 +2455,17 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   OCTSAM_CHECK_ARG(!want_cs || (a->a_mode == 1 && a->b_mode == 1), "octsam_gemm: a_colsum / b_colsum need a_mode = b_mode = 1");
   {  // lean epilogue kind (epilogue_fast): no C_pre; a residual must have C's type, no broadcast (r_blk)
     const int es = a->c_f32 ? 4 : 2;
-    const bool res_ok = a->R == nullptr || (a->r_f32 == a->c_f32 && (a->r_blk == 0 || a->row_map == nullptr) &&
+    // (an fp32 residual under an e16 C: the broadcast kind only -- the decoder's first block adds the fp32 image
+    //  embedding to its per-prompt keys)
+    const bool r_mixed = a->R && a->r_f32 && !a->c_f32 && a->r_blk > 0 && a->row_map == nullptr;
+    const bool res_ok = a->R == nullptr || ((a->r_f32 == a->c_f32 || r_mixed) && (a->r_blk == 0 || a->row_map == nullptr) &&
                                             (a->ldr & 7) == 0 && ((uintptr_t)a->R & 15) == 0);
     const long long rows = a->row_map ? (long long)a->c_rows : (long long)a->M;
     const bool range_ok = rows > 0 && rows * a->ldc * es < (1LL << 31) &&
-                          (a->R == nullptr || rows * a->ldr * es < (1LL << 31));
+                          (a->R == nullptr || rows * a->ldr * (a->r_f32 ? 4 : 2) < (1LL << 31));
     k.fast_epi = (a->C_pre == nullptr && (a->ldc & 7) == 0 && ((uintptr_t)a->C & 15) == 0 && res_ok && range_ok)
                      ? 1 + (a->c_f32 ? 1 : 0) + (a->R ? 2 : 0) + (a->row_map ? 4 : 0) +
-                           (a->R && a->r_blk > 0 ? 8 : 0)
+                           (a->R && a->r_blk > 0 ? 8 : 0) + (r_mixed ? 16 : 0)
                      : 0;
     k.c_rows = a->c_rows;
     if (g_use_glds == 18) k.fast_epi = 0;  // diagnostics / parity: the general register epilogue

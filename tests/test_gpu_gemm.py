@@ -630,6 +630,31 @@ def test_gemm4w_broadcast_residual(cuda, N):
     assert torch.equal(outs[0], outs[1])
 
 
+def test_gemm8_f32_broadcast_residual_under_e16(cuda):
+    """Lean kind 27 (e16 C + a broadcast fp32 residual: the first two-way block's image-side out_proj, whose keys
+    residual is the fp32 image embedding shared by the image's prompts) against torch fp32 and bit-identical to the
+    general register epilogue it replaces (fast path 18)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    L, B, rep, N, K = 4096, 2, 3, 256, 128
+    M = L * B * rep
+    g = torch.Generator().manual_seed(27)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(B * L, N, generator=g).to(cuda)
+    outs = []
+    for fast in (1, 18):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, residual=R, ldr=N, r_remap=(L, rep))
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    ref = A.float() @ W.float().t() + bias + R.view(B, 1, L, N).expand(B, rep, L, N).reshape(M, N)
+    assert _rel(outs[0], ref) < 5e-3
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm4w_patch_embed_kind(cuda):
     """The patch embedding's GEMM (fp32 encoder stream out, bias, the positional table as a periodic fp32 addend:
     lean kind 12) on the two-workgroup kernel against torch fp32 and bit-identical to the 8-phase kernel's general
