@@ -106,6 +106,9 @@ _SIGNATURES = {
     "octsam_dec_i2t_fwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                      c_void_p, c_int64, c_void_p]),
     "octsam_dec_i2t_bwd_partials": (c_int64, [c_int32, c_int32, c_int32]),
+    "octsam_dec_i2t_bwd_sum_partials": (c_int64, [c_int32, c_int32, c_int32]),
+    "octsam_dec_i2t_bwd_sum": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                         c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "octsam_dec_i2t_bwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                      c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "octsam_upmask_fwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),

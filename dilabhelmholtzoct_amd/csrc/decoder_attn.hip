@@ -763,6 +763,186 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
   }
 }
 
+// Backward of the shared-query form (q_rep > 1: the first block's image-side queries are the image embedding, shared
+// by the image's q_rep prompts) with the prompt sum of dQ fused in: a workgroup = (image, 64-row chunk), wave = head
+// pair; the chunk's query rows are staged once, each prompt's dO rows stream through a two-prompt LDS ring (the next
+// prompt's rows and token operands load while the current prompt computes), dQ of the chunk accumulates over the
+// prompts in fp32 registers and is stored once per image -- the per-prompt [P*L, CI] dQ and its prompt-sum pass never
+// touch HBM. dK / dV partials per (chunk, prompt) as in i2t_bwd_kernel.
+namespace i2s {
+constexpr int SCH = 64;                                  // rows per workgroup chunk (2 steps)
+constexpr int Q_BYTES = 2 * 2048, D_BYTES = 2 * 2048;    // query rows / one prompt's dO rows, 2 steps of 32 rows
+constexpr int WAVE_LDS = Q_BYTES + 2 * D_BYTES;          // 12 KiB per wave
+constexpr int SMEM = 4 * WAVE_LDS;
+}  // namespace i2s
+
+// 32 rows (r0 ..) of a head pair's 64-B slices -> a 2 KiB image (vimg: the V-image swizzle, else the K-image one)
+__device__ __forceinline__ void load_rows32(const bf16* b, long long ld, int r0, char* dst, bool vimg, int lane) {
+  using namespace t2;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * i + (lane >> 2), pc = lane & 3;
+    __builtin_amdgcn_global_load_lds((const void*)(b + (long long)(r0 + r) * ld + 8 * (vimg ? vsw(r, pc) : ksw(r, pc))),
+                                     (lds_ptr_t)(dst + 1024 * i), 16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict__ q, long long ldq, int q_rep,
+                                                          const float* __restrict__ k, const float* __restrict__ v,
+                                                          int Tk, int L, int nchunk, const bf16* __restrict__ dout,
+                                                          long long lddo, bf16* __restrict__ dq, long long lddq,
+                                                          float* __restrict__ part, int P) {
+  using namespace t2;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int img = blockIdx.x / nchunk, chunk = blockIdx.x - img * nchunk;
+  const int r0 = chunk * i2s::SCH;
+  char* qimg = tsm + hp * i2s::WAVE_LDS;
+  char* dring = qimg + i2s::Q_BYTES;
+  const bf16* qb = q + (long long)img * L * ldq + hp * 32;
+  const int p0 = img * q_rep;
+  auto dbase = [&](int p) { return dout + (long long)p * L * lddo + hp * 32; };
+  load_rows32(qb, ldq, r0, qimg, false, lane);
+  load_rows32(qb, ldq, r0 + STEP, qimg + 2048, false, lane);
+  load_rows32(dbase(p0), lddo, r0, dring, true, lane);
+  load_rows32(dbase(p0), lddo, r0 + STEP, dring + 2048, true, lane);
+  // token operands of one prompt, raw fp32 (tok_op / tokT_op's elements), so the next prompt's loads overlap
+  struct Raw {
+    float kv[8], vv[8], kT[2][4];
+  };
+  auto load_raw = [&](int p, Raw& r) {
+    const int qi = c & 7;
+    const bool on = (g >> 1) == (c >> 3) && qi < Tk;
+    const float* ks = k + ((long long)p * Tk + (on ? qi : 0)) * 128 + hp * 32 + 8 * g;
+    const float* vs = v + ((long long)p * Tk + (on ? qi : 0)) * 128 + hp * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r.kv[j] = on ? ks[j] : 0.0f;
+      r.vv[j] = on ? vs[j] : 0.0f;
+    }
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 4 * g + j, qj = n & 7;
+        const bool o2 = (n >> 3) == hl && qj < Tk;
+        r.kT[hl][j] = o2 ? k[((long long)p * Tk + qj) * 128 + (2 * hp + hl) * 16 + c] : 0.0f;
+      }
+  };
+  bool nv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) nv[i] = ((4 * g + i) & 7) < Tk;
+  const bool cv = (c & 7) < Tk;
+  f32x4 adq[2][2][2];  // [step][16-row half][head of the pair]
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) adq[s2][t][hl] = (f32x4)0.0f;
+  Raw cur, nxt;
+  load_raw(p0, cur);
+  for (int pi = 0; pi < q_rep; ++pi) {
+    const int p = p0 + pi;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this prompt's rows (and operands) landed
+    __builtin_amdgcn_wave_barrier();
+    if (pi + 1 < q_rep) {  // the next prompt's dO rows into the other buffer (read two iterations ago), its operands
+      char* nb = dring + ((pi + 1) & 1) * i2s::D_BYTES;
+      load_rows32(dbase(p + 1), lddo, r0, nb, true, lane);
+      load_rows32(dbase(p + 1), lddo, r0 + STEP, nb + 2048, true, lane);
+      load_raw(p + 1, nxt);
+    }
+    bf16x8 khi, klo, vop;
+    const float ks = 0.25f * L2E;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = cur.kv[j] * ks;
+      khi[j] = (bf16)x;
+      klo[j] = (bf16)(x - (float)khi[j]);
+      vop[j] = (bf16)cur.vv[j];
+    }
+    s16x4 ak[2];
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ak[hl][j] = __builtin_bit_cast(short, (bf16)(cur.kT[hl][j] * 0.25f));
+    f32x4 dka[2], dva[2];
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) dka[hl] = dva[hl] = (f32x4)0.0f;
+    const char* dcur = dring + (pi & 1) * i2s::D_BYTES;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const char* slot = qimg + s2 * 2048;
+      const char* dimg = dcur + s2 * 2048;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8 qf = row_op(slot, t, false, lane), df = row_op(dimg, t, true, lane);
+        f32x4 sT = mfma32(khi, qf, (f32x4)0.0f);
+        sT = mfma32(klo, qf, sT);
+        const f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, sT[i]) : mx;
+        mx = max_xor16(mx);
+        f32x4 pT;
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pT[i] = nv[i] ? __builtin_amdgcn_exp2f(sT[i] - mx) : 0.0f;
+          sum += pT[i];
+        }
+        sum = add_xor16(sum);
+        const float inv = 1.0f / sum;
+        float del = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pT[i] *= inv;
+          del = fmaf(pT[i], dpT[i], del);
+        }
+        del = add_xor16(del);
+        f32x4 dsT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dsT[i] = pT[i] * (dpT[i] - del);
+        const s16x4 dsTb = pack4(dsT);
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) adq[s2][t][hl] = mfma16(ak[hl], dsTb, adq[s2][t][hl]);
+        f32x4 sS = mfma32(qf, khi, (f32x4)0.0f);
+        sS = mfma32(qf, klo, sS);
+        const f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+        f32x4 pS, dsS;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int src = 32 * (c >> 3) + 4 * g + i;
+          const float Mi = __shfl(mx, src, 64), Ii = __shfl(inv, src, 64), Di = __shfl(del, src, 64);
+          pS[i] = cv ? __builtin_amdgcn_exp2f(sS[i] - Mi) * Ii : 0.0f;
+          dsS[i] = pS[i] * (dpS[i] - Di);
+        }
+        const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          dka[hl] = mfma16(tr_op(slot, t, hl, false, lane), dsSb, dka[hl]);
+          dva[hl] = mfma16(tr_op(dimg, t, hl, true, lane), pSb, dva[hl]);
+        }
+      }
+    }
+    if (cv) {
+      const int hl = c >> 3, j = c & 7, h = 2 * hp + hl;
+      float* w = part + (((long long)chunk * P + p) * 2) * Tk * 128 + j * 128 + h * 16 + 4 * g;
+      *(f32x4*)w = (hl ? dka[1] : dka[0]) * 0.25f;
+      *(f32x4*)(w + Tk * 128) = hl ? dva[1] : dva[0];
+    }
+    if (pi + 1 < q_rep) cur = nxt;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16* dqr = dq + ((long long)img * L + r0 + s2 * STEP + 16 * t + c) * lddq + hp * 32 + 4 * g;
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) *(s16x4*)(dqr + 16 * hl) = pack4(adq[s2][t][hl]);
+    }
+}
+
 }  // namespace
 
 extern "C" int octsam_dec_tok_attn_fwd(const float* q, const float* k, const float* v, int32_t P, int32_t T, void* out,
@@ -910,5 +1090,30 @@ extern "C" int octsam_dec_i2t_bwd(const void* q, int64_t ldq, int32_t q_rep, con
   hipLaunchKernelGGL(i2t_bwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, (hipStream_t)stream, (const bf16*)q, ldq,
                      q_rep, k, v, Tk, L, nch, (const bf16*)dout, lddo, (bf16*)dq, lddq, partials, P);
   OCTSAM_LAUNCH_CHECK("octsam_dec_i2t_bwd");
+  return 0;
+}
+
+// the shared-query backward with the prompt sum of dQ fused in (i2t_bwd_sum_kernel): dq holds the IMAGE rows
+// [(P / q_rep) * L, lddq]; dK / dV partials: octsam_dec_i2t_bwd_sum_partials(P, Tk, L) floats, reduced by the caller
+extern "C" int64_t octsam_dec_i2t_bwd_sum_partials(int32_t P, int32_t Tk, int32_t L) {
+  return (int64_t)(L / i2s::SCH) * P * 2 * Tk * 128;
+}
+
+extern "C" int octsam_dec_i2t_bwd_sum(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v,
+                                      int32_t P, int32_t Tk, int32_t L, const void* dout, int64_t lddo, void* dq,
+                                      int64_t lddq, float* partials, void* stream) {
+  OCTSAM_CHECK_ARG(q && k && v && dout && dq && partials && P > 0 && Tk > 0 && Tk <= MAXT && L > 0 &&
+                       L % i2s::SCH == 0 && q_rep > 0 && P % q_rep == 0 && ldq % 8 == 0 && lddo % 8 == 0 &&
+                       lddq % 4 == 0 && (uintptr_t)q % 16 == 0 && (uintptr_t)dout % 16 == 0 && (uintptr_t)dq % 8 == 0,
+                   "octsam_dec_i2t_bwd_sum: bad args");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)i2t_bwd_sum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, i2s::SMEM);
+    attr = true;
+  }
+  const int nch = L / i2s::SCH, nimg = P / q_rep;
+  hipLaunchKernelGGL(i2t_bwd_sum_kernel, dim3(nimg * nch), dim3(256), i2s::SMEM, (hipStream_t)stream, (const bf16*)q,
+                     ldq, q_rep, k, v, Tk, L, nch, (const bf16*)dout, lddo, (bf16*)dq, lddq, partials, P);
+  OCTSAM_LAUNCH_CHECK("octsam_dec_i2t_bwd_sum");
   return 0;
 }

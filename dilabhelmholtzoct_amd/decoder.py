@@ -280,8 +280,9 @@ class MaskDecoder(nn.Module):
     # token-side weight + bias gradients through octsam_wgrad_tok (False: split-K tile GEMM + reduction + column-sum
     # kernel + reduction; A/B, scripts/step_ab3.py)
     tok_wgrad = True
-    # the first block's token->image backward with the prompt sum of its shared K / V gradients fused in
-    # (octsam_dec_t2i_bwd_sum; False: per-prompt gradients + octsam_group_sum; A/B, scripts/step_ab3.py)
+    # the first block's attention backwards with the prompt sums of their image-shared operands' gradients fused in
+    # (token->image K / V: octsam_dec_t2i_bwd_sum; image->token Q: octsam_dec_i2t_bwd_sum; False: per-prompt gradients
+    # + octsam_group_sum; A/B, scripts/step_ab3.py)
     t2i_sum = True
     # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
@@ -704,7 +705,13 @@ class MaskDecoder(nn.Module):
             self._lin_bwd(ds4_b, ls.i2t_o_b, i2t + "out_proj.weight", i2t + "out_proj.bias", RL, dx_out=dio_b)
             # i2t attention
             KQV = ls.KQV
-            if li == 0:
+            dQ_img = None
+            if li == 0 and self.t2i_sum and ls.kv_rep > 1 and L % 64 == 0:
+                # queries shared by the image's prompts: their gradient summed over the prompts inside the kernel
+                dQ_img = torch.empty(B * L, CI, device=dev, dtype=b16)
+                dKt, dVt = K.i2t_bwd_sum(KQV[:, CI:], 3 * CI, ls.kv_rep, ls.i2t_K, ls.i2t_V, P, T, L, dio_b, CI,
+                                         dQ_img, CI)
+            elif li == 0:
                 dQp = torch.empty(RL, CI, device=dev, dtype=b16)
                 dKt, dVt = K.i2t_bwd(KQV[:, CI:], 3 * CI, ls.kv_rep, ls.i2t_K, ls.i2t_V, P, T, L, dio_b, CI, dQp, CI)
             else:
@@ -755,8 +762,9 @@ class MaskDecoder(nn.Module):
                     dV_img = torch.empty(Mi, CI, device=dev, dtype=b16)
                     K.group_sum(dKV0, dK_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
                     K.group_sum(dKV0[:, CI:], dV_img, ld_in=2 * CI, cols=CI, groups=B, nper=N, rows_per=L)
-                dQ_img = torch.empty(Mi, CI, device=dev, dtype=b16)
-                K.group_sum(dQp, dQ_img, ld_in=CI, cols=CI, groups=B, nper=N, rows_per=L)
+                if dQ_img is None:
+                    dQ_img = torch.empty(Mi, CI, device=dev, dtype=b16)
+                    K.group_sum(dQp, dQ_img, ld_in=CI, cols=CI, groups=B, nper=N, rows_per=L)
                 self._dw(dK_img, s.imgd_b, Mi, self.G(t2i + "k_proj.weight"), ldy=ldkv, x_add=s.pe_b, x_add_rows=L,
                          db=self.G(t2i + "k_proj.bias"))
                 self._dw(dQ_img, s.imgd_b, Mi, self.G(i2t + "q_proj.weight"), x_add=s.pe_b, x_add_rows=L,

@@ -353,6 +353,21 @@ def i2t_bwd(q, ldq, q_rep, k, v, P, Tk, L, dout, lddo, dq, lddq):
     return red[:, 0], red[:, 1]
 
 
+def i2t_bwd_sum(q, ldq, q_rep, k, v, P, Tk, L, dout, lddo, dq, lddq):
+    """i2t_bwd for queries shared by q_rep prompts per image with the prompt sum of dQ fused in: dq holds the image
+    rows [(P / q_rep) * L, lddq] (octsam_dec_i2t_bwd_sum). Returns dk, dv fp32 [P, Tk, 128] each."""
+    _require_cuda(q, k, v, dout, dq)
+    n = _lib.load().octsam_dec_i2t_bwd_sum_partials(P, Tk, L)
+    nb = n // (P * 2 * Tk * 128)
+    part = torch.empty(n, device=k.device, dtype=torch.float32)
+    _lib.call("octsam_dec_i2t_bwd_sum", ptr(q), ldq, q_rep, ptr(k), ptr(v), P, Tk, L, ptr(dout), lddo, ptr(dq), lddq,
+              ptr(part))
+    red = torch.empty(P * 2 * Tk * 128, device=k.device, dtype=torch.float32)
+    splitk_reduce(part.view(nb, -1), red, nb)
+    red = red.view(P, 2, Tk, 128)
+    return red[:, 0], red[:, 1]
+
+
 def upmask_fwd(up1, w2, b2, hyper, P, ntok, masks):
     """Fused ConvT2 + GELU + mask head (octsam_upmask_fwd): masks [P, ntok, 256, 256] fp32."""
     _require_cuda(up1, w2, b2, hyper, masks)

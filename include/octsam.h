@@ -289,6 +289,14 @@ int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t
 int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
                        int32_t L, void* out, int64_t ldo, void* stream);
 int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L);
+/* octsam_dec_i2t_bwd for queries shared by q_rep prompts per image (the first two-way block's image-side queries)
+ * with the prompt sum of dQ fused in: dq holds the IMAGE rows [(P / q_rep) * L, lddq] = the sum over the image's
+ * prompts, accumulated in fp32 (replaces the per-prompt [P * L] rows + octsam_group_sum). L % 64 == 0; dK / dV
+ * partials as octsam_dec_i2t_bwd's, octsam_dec_i2t_bwd_sum_partials(P, Tk, L) elements (ABI 20). */
+int64_t octsam_dec_i2t_bwd_sum_partials(int32_t P, int32_t Tk, int32_t L);
+int octsam_dec_i2t_bwd_sum(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P,
+                           int32_t Tk, int32_t L, const void* dout, int64_t lddo, void* dq, int64_t lddq,
+                           float* partials, void* stream);
 int octsam_dec_i2t_bwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
                        int32_t L, const void* dout, int64_t lddo, void* dq, int64_t lddq, float* partials,
                        void* stream);

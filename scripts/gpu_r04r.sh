@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4: the first block's image->token backward with the prompt sum of dQ fused in: parity tests, step A/B.
+set -u
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-r04r}; mkdir -p $O; cd $R
+timeout -k 10 500 python -u -m pytest -x -v --timeout 280 --timeout-method thread tests/test_gpu_dec_attn.py tests/test_gpu_model.py tests/test_gpu_graph_step.py tests/test_gpu_pipeline.py > $O/pytest_r.log 2>&1 || { tail -30 $O/pytest_r.log; exit 1; }
+tail -1 $O/pytest_r.log
+STEP_VARIANTS=default,t2isum_off timeout -k 10 400 python -u scripts/step_ab3.py > $O/step_ab_sum.log 2>&1 || { tail -20 $O/step_ab_sum.log; exit 1; }
+tail -1 $O/step_ab_sum.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/profseq -o run -- python3 $R/bench.py --pipeline 0 --cpu-baseline 0 --val 0 --val-protocol 0 --top-off 0 --data-path 0 --e2e-steps 0 --topo-all 0 --loop-images 0 > $O/profseq.log 2>&1 || { tail -5 $O/profseq.log; exit 1; }
+python3 $R/scripts/prof_summary.py $O/profseq $O/kernel_stats_sequential.csv --delete-trace || exit 1
+grep -E "i2t_bwd|group_sum" $O/kernel_stats_sequential.csv | cut -c1-60,150-

@@ -137,6 +137,38 @@ def test_i2t_fwd_bwd(cuda, P, q_rep, T, ldq):
     assert _rel(dv, vr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("P,q_rep,T,ldq", [(6, 3, 7, 384), (21, 21, 7, 384), (4, 2, 4, 128), (4, 4, 1, 384)])
+def test_i2t_bwd_sum(cuda, P, q_rep, T, ldq):
+    """The shared-query backward with the prompt sum of dQ fused in (octsam_dec_i2t_bwd_sum: image-row dQ summed over
+    the image's prompts in fp32) vs torch fp32 autograd, vs the per-prompt kernel summed afterwards, dK / dV vs the
+    per-prompt kernel's (same per-prompt arithmetic, another chunk partition of the fp32 sums); bitwise repeatable."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(P * 11 + q_rep + T)
+    B = P // q_rep
+    qbuf = (torch.randn(B * L, ldq, generator=g) * 1.5).to(cuda, torch.bfloat16)
+    k = (torch.randn(P, T, CI, generator=g) * 2).to(cuda)
+    v = torch.randn(P, T, CI, generator=g).to(cuda)
+    qr = qbuf[:, :CI].float().reshape(B, L, CI).requires_grad_()
+    kr = k.clone().requires_grad_()
+    vr = v.clone().requires_grad_()
+    oref = _i2t_ref(qr, kr, vr, q_rep)
+    dout = torch.randn(P, L, CI, generator=g).to(cuda, torch.bfloat16)
+    oref.backward(dout.float())
+    dq = torch.empty(B * L, CI, device=cuda, dtype=torch.bfloat16)
+    dk, dv = kernels.i2t_bwd_sum(qbuf, ldq, q_rep, k, v, P, T, L, dout, CI, dq, CI)
+    assert _rel(dq.float().reshape(B, L, CI), qr.grad) < 2e-2
+    assert _rel(dk, kr.grad) < 2e-2
+    assert _rel(dv, vr.grad) < 2e-2
+    dq1 = torch.empty(P * L, CI, device=cuda, dtype=torch.bfloat16)
+    dk1, dv1 = kernels.i2t_bwd(qbuf, ldq, q_rep, k, v, P, T, L, dout, CI, dq1, CI)
+    assert _rel(dq, dq1.float().reshape(B, q_rep, L, CI).sum(1).reshape(B * L, CI)) < 1e-2
+    # (fp32 sums over 64 chunks instead of 8, with cancellation: ~3e-4 of the max measured)
+    assert _rel(dk, dk1) < 2e-3 and _rel(dv, dv1) < 2e-3
+    dq2 = torch.empty_like(dq)
+    dk2, dv2 = kernels.i2t_bwd_sum(qbuf, ldq, q_rep, k, v, P, T, L, dout, CI, dq2, CI)
+    assert torch.equal(dq2, dq) and torch.equal(dk2, dk) and torch.equal(dv2, dv)
+
+
 def test_t2i_deterministic(cuda):
     """Fixed-order reductions: two runs give identical bits."""
     from dilabhelmholtzoct_amd import kernels
