@@ -582,13 +582,18 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
     }
   }
   __syncthreads();
-  // creator cells -> top-dimensional cofaces and their values
+  // creator cells -> top-dimensional cofaces and their values; the high word of each persistence's order-preserving
+  // bit image (keys are dead: the records hold what the ranking needs) decides most comparisons of the ranking
+  uint32_t* phi = (uint32_t*)s.keys;
   for (int d = 0; d < 2; ++d) {
     const int n = min(s.nrec[d], rec_cap(d)), o = rec_base(d);
     for (int i = tid; i < n; i += NTHR) {
       const int c = top_coface(m, s.u.rec.c[o + i]);
       s.u.rec.c[o + i] = c;
-      s.u.rec.pers[o + i] = (double)unord_bits((uint32_t)(s.u.rec.key[o + i] >> 32)) - (double)s.vals[c];
+      const double p = (double)unord_bits((uint32_t)(s.u.rec.key[o + i] >> 32)) - (double)s.vals[c];
+      s.u.rec.pers[o + i] = p;
+      const uint64_t b = (uint64_t)__double_as_longlong(p + 0.0);  // (-0 -> +0: equal values, equal images)
+      phi[o + i] = (uint32_t)(((int64_t)b < 0 ? ~b : b | 0x8000000000000000ull) >> 32);
     }
   }
   __syncthreads();
@@ -609,11 +614,29 @@ __global__ __launch_bounds__(NTHR) void cubical_ph_kernel(const float* __restric
       const uint64_t ki = s.u.rec.key[o + i];
       const int ci = s.u.rec.c[o + i];
       const double pi = s.u.rec.pers[o + i];
+      const uint32_t hi = phi[o + i];  // >= 2^31 (the image of a non-negative value); 0 marks past-n slots below
       int rank = 0;
-#pragma unroll 4
-      for (int j = 0; j < n; ++j) {
-        const double pj = s.u.rec.pers[o + j];
-        rank += (pj > pi) || (pj == pi && s.u.rec.key[o + j] < ki);
+      // 8 images per trip, loaded together: distinct images decide (the image order is the persistence order);
+      // equal images (ties of the high word: rare but for binary maps) take the exact (persistence, key) compare on
+      // a wave-uniform branch
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        uint32_t hv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hv[u] = j0 + u < n ? phi[o + j0 + u] : 0u;
+        bool tie = false;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          rank += hv[u] > hi;
+          tie |= hv[u] == hi;
+        }
+        if (__builtin_amdgcn_ballot_w64(tie)) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (hv[u] == hi) {
+              const double pj = s.u.rec.pers[o + j0 + u];
+              rank += (pj > pi) || (pj == pi && s.u.rec.key[o + j0 + u] < ki);
+            }
+        }
       }
       if (rank < max_pairs) {
         const int pos = (int)(uint32_t)ki;
