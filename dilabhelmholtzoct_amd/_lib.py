@@ -117,6 +117,8 @@ _SIGNATURES = {
     "octsam_upmask_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_upmask_ln_bwd": (c_int32, [c_void_p] * 5 + [c_int32, c_int32] + [c_void_p] * 13),
+    "octsam_upmask_ln_bwd_strided": (c_int32, [c_void_p] * 5 + [c_int32, c_int32] + [c_void_p] * 6 + [c_int64] +
+                                     [c_void_p] * 7),
     "octsam_postproc_fwd": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                       c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     "octsam_dice_partials": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_int32, c_void_p]),

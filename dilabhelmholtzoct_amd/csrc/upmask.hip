@@ -281,6 +281,7 @@ struct LnArgs {
   const float* w;
   const float* b;
   float* part;
+  long long ldd;  // d up1 / d x: elements between the [P * 4096, 256] rows (4 [.., 64] rows each); 256 = contiguous
 };
 // part_h fp32 [256][P * NS * 32] (per tile-in-prompt), part_w [grid][64][128], part_b [grid][32]
 template <int NS, bool LN>
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
         bf16x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (bf16)(rs * (gy[4 * kb + i] * lw[i] - s1 - xnorm(kb, i) * s2));
-        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
+        *(bf16x4*)(dup1 + (orow >> 2) * ln.ldd + (orow & 3) * 64 + 16 * kb + 4 * g) = o;
       }
     } else {
       const long long orow = (long long)T * BROWS + rr;
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(256, 2) void upmask_bwd_kernel(const bf16* __restri
         bf16x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (bf16)da[kb][i];
-        *(bf16x4*)(dup1 + orow * 64 + 16 * kb + 4 * g) = o;
+        *(bf16x4*)(dup1 + (orow >> 2) * ln.ldd + (orow & 3) * 64 + 16 * kb + 4 * g) = o;
       }
     }
     __syncthreads();  // (C) dpre tile and d hyper rows complete
@@ -599,12 +600,13 @@ extern "C" int64_t octsam_upmask_bwd_workspace(int32_t P, int32_t ntok) {
 namespace {
 int upmask_bwd_impl(const void* up1, const void* w2, const float* b2, const float* hyper, const float* dmask, int32_t P,
                     int32_t ntok, void* dout, float* dw2, float* db2, float* dhyper, float* workspace, const LnArgs* ln,
-                    float* dlnw, float* dlnb, void* stream) {
+                    float* dlnw, float* dlnb, void* stream, long long ldd = 256) {
   const int ntiles = P * um::BTILES_PER_P, grid = upmask_grid(ntiles, g_bwd_grid);
   float* part_h = workspace;
   float* part_w = part_h + (long long)um::BTILES_PER_P * P * ntok * 32;
   float* part_b = part_w + (long long)grid * 8192;
-  LnArgs la = ln ? *ln : LnArgs{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  LnArgs la = ln ? *ln : LnArgs{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 256};
+  la.ldd = ldd;
   la.part = part_b + (long long)grid * 32 + (long long)grid * 256;  // [2][grid][64]
   hipStream_t s = (hipStream_t)stream;
   const int lds = um::S_DM + ntok * 1024 + 4 * ntok * 32 * 4 + (ln ? (128 + 512) * 4 : 0);
@@ -651,7 +653,28 @@ extern "C" int octsam_upmask_ln_bwd(const void* up1, const void* w2, const float
   OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
                        ((uintptr_t)dx & 7) == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
                    "octsam_upmask_ln_bwd: misaligned operand");
-  const LnArgs ln{(const bf16*)x, mean, rstd, ln_w, ln_b, nullptr};
+  const LnArgs ln{(const bf16*)x, mean, rstd, ln_w, ln_b, nullptr, 256};
   return upmask_bwd_impl(up1, w2, b2, hyper, dmask, P, ntok, dx, dw2, db2, dhyper, workspace, &ln, dln_w, dln_b,
                          stream);
+}
+
+// octsam_upmask_ln_bwd writing d x with a row stride: row r of the [P * 4096, 256] view at dx + r * ldx (ldx >= 256,
+// a multiple of 4), so d x can be the left half of a wider operand (decoder.py: [d x | d keys of the final attention]
+// feed ONE keys-gradient product)
+extern "C" int octsam_upmask_ln_bwd_strided(const void* up1, const void* w2, const float* b2, const float* hyper,
+                                            const float* dmask, int32_t P, int32_t ntok, const void* x,
+                                            const float* mean, const float* rstd, const float* ln_w,
+                                            const float* ln_b, void* dx, int64_t ldx, float* dw2, float* db2,
+                                            float* dhyper, float* dln_w, float* dln_b, float* workspace,
+                                            void* stream) {
+  OCTSAM_CHECK_ARG(up1 && w2 && b2 && hyper && dmask && x && mean && rstd && ln_w && ln_b && dx && dw2 && db2 &&
+                       dhyper && dln_w && dln_b && workspace && P > 0 && (ntok == 1 || ntok == 3) && ldx >= 256 &&
+                       ldx % 4 == 0,
+                   "octsam_upmask_ln_bwd_strided: bad args (ntok 1 or 3, ldx >= 256 and a multiple of 4)");
+  OCTSAM_CHECK_ARG(((uintptr_t)up1 & 15) == 0 && ((uintptr_t)hyper & 15) == 0 && ((uintptr_t)dmask & 15) == 0 &&
+                       ((uintptr_t)dx & 7) == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)workspace & 15) == 0,
+                   "octsam_upmask_ln_bwd_strided: misaligned operand");
+  const LnArgs ln{(const bf16*)x, mean, rstd, ln_w, ln_b, nullptr, 256};
+  return upmask_bwd_impl(up1, w2, b2, hyper, dmask, P, ntok, dx, dw2, db2, dhyper, workspace, &ln, dln_w, dln_b,
+                         stream, ldx);
 }

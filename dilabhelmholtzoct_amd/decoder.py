@@ -284,6 +284,9 @@ class MaskDecoder(nn.Module):
     # (token->image K / V: octsam_dec_t2i_bwd_sum; image->token Q: octsam_dec_i2t_bwd_sum; False: per-prompt gradients
     # + octsam_group_sum; A/B, scripts/step_ab3.py)
     t2i_sum = True
+    # the keys gradient of the mask head and the final attention as one product over [d up1pre | dK | dV] (False:
+    # two products, the second read-modify-writing d keys2; A/B, scripts/step_ab3.py)
+    fuse_dkeys = True
     # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
     fused_ln_bwd = True
@@ -367,14 +370,15 @@ class MaskDecoder(nn.Module):
             K.splitk_reduce(pb.view(split * dbx_fold, -1), dbx, split * dbx_fold)
         return out
 
-    def _dw_pe(self, dy, x, M, out, n_pe, pe_b, db=None):
+    def _dw_pe(self, dy, x, M, out, n_pe, pe_b, db=None, ldy=None):
         """Weight gradient of _proj_pe: out[o, i] = sum_m dy[m, o] x[m, i] for every grouped row o (one
         k-major GEMM over the M rows), plus sum_p S[p, o] pe[p, i] for the first n_pe rows, S[p] = sum_j
         dy[j*4096 + p] (the PE term); db (optional) = sum_m dy[m, o], fused into the GEMM."""
         O = out.shape[0]
-        self._dw(dy, x, M, out, ldy=O, db=db)
+        ldy = O if ldy is None else ldy
+        self._dw(dy, x, M, out, ldy=ldy, db=db)
         S = torch.empty(L_IMG, n_pe, device=out.device, dtype=torch.bfloat16)
-        K.group_sum(dy, S, ld_in=O, cols=n_pe, groups=1, nper=M // L_IMG, rows_per=L_IMG)
+        K.group_sum(dy, S, ld_in=ldy, cols=n_pe, groups=1, nper=M // L_IMG, rows_per=L_IMG)
         self._dw(S, pe_b, L_IMG, out[:n_pe], ldy=n_pe, accumulate=True)
         return out
 
@@ -633,13 +637,18 @@ class MaskDecoder(nn.Module):
         # ---- mask head + ConvT2 (+ GELU), fused: recomputes the ConvT2 product from up1; with fused_ln_bwd the
         # LayerNorm2d + GELU backward rides in the same pass (d up1 never reaches HBM)
         dhyper = torch.empty(P, nsel, 32, device=dev, dtype=f32)
-        dup1pre = torch.empty(RL * 4, 64, device=dev, dtype=b16)
+        # joint: d up1pre is the left half of one [RL, 512] operand whose right half receives the final attention's
+        # [dK | dV], so the keys gradient d keys2 = [d up1pre | dK | dV] @ [W1; Wk; Wv] is ONE product (no in-place
+        # read-modify-write of d keys2 by a second one)
+        joint = self.fuse_dkeys and self.fused_ln_bwd
+        dup_ld = 512 if joint else 256
+        dup1pre = torch.empty(RL, dup_ld, device=dev, dtype=b16)
         lnw, lnb = self.Bf("upscale_layer_norm.weight"), self.Bf("upscale_layer_norm.bias")
         glnw, glnb = self.G("upscale_layer_norm.weight"), self.G("upscale_layer_norm.bias")
         if self.fused_ln_bwd:
             K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel,
                          dup1pre, self.G("upscale_conv2.weight"), self.G("upscale_conv2.bias"), dhyper,
-                         ln=(s.up1pre, s.up_mean, s.up_rstd, lnw, lnb, glnw, glnb))
+                         ln=(s.up1pre, s.up_mean, s.up_rstd, lnw, lnb, glnw, glnb), ldd=dup_ld)
         else:
             dup1 = torch.empty(RL * 4, 64, device=dev, dtype=b16)
             K.upmask_bwd(s.up1, self.W("upscale_conv2.weight"), self.Bf("upscale_conv2.bias"), s.hyper, dm, P, nsel,
@@ -649,9 +658,10 @@ class MaskDecoder(nn.Module):
         # the image-side keys gradient stream is bf16 (as under the reference's bf16 autocast): it is written,
         # read-modify-written by each block's projection backward and read by LayerNorm4's backward per block
         dkeys = torch.empty(RL, C, device=dev, dtype=b16)
-        K.gemm(dup1pre, self.W("upscale_conv1.weight"), M=RL, N=C, K=256, out=dkeys, b_mode=0)
+        if not joint:
+            K.gemm(dup1pre, self.W("upscale_conv1.weight"), M=RL, N=C, K=256, out=dkeys, b_mode=0)
         # (bias: column sums of dup1pre's [RL, 4 x 64] view, folded over the 4 ConvT taps)
-        self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=256,
+        self._dw(s.keys2_b, dup1pre, RL, self.G("upscale_conv1.weight"), ldy=C, ldx=dup_ld,
                  dbx=self.G("upscale_conv1.bias"), dbx_fold=4)
         # ---- hypernetwork MLP backward -> dq7
         dq7 = torch.zeros(R, C, device=dev, dtype=f32)
@@ -677,15 +687,21 @@ class MaskDecoder(nn.Module):
         dfo = torch.empty(R, CI, device=dev, dtype=f32)
         self._lin_bwd(dsf_b, s.f_o_b, f + "out_proj.weight", f + "out_proj.bias", R, dx_out=dfo)
         dQ = torch.empty(R, CI, device=dev, dtype=b16)
-        dKV = torch.empty(RL, 2 * CI, device=dev, dtype=b16)
-        K.t2i_bwd(s.f_Q, s.f_KV, s.f_KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, dfo, s.f_lse, dQ, dKV, dKV[:, CI:],
-                  2 * CI)
+        if joint:
+            dKV, lkv = dup1pre[:, 256:], 512
+        else:
+            dKV, lkv = torch.empty(RL, 2 * CI, device=dev, dtype=b16), 2 * CI
+        K.t2i_bwd(s.f_Q, s.f_KV, s.f_KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, dfo, s.f_lse, dQ, dKV, dKV[:, CI:], lkv)
         self._qin_bwd(dQ, s.f_qin_b, f + "q_proj.weight", f + "q_proj.bias", R, dq, dtok)
         # d keys2 += [dK | dV] @ [Wk; Wv]
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
-        self._dx(dKV, wkv, RL, dkeys, beta=1.0)
+        if joint:  # d keys2 = [d up1pre | dK | dV] @ [W1; Wk; Wv], one product (B [C, 512]: B[n][k])
+            bcat = torch.cat([self.W("upscale_conv1.weight"), wkv.t()], 1).contiguous()
+            K.gemm(dup1pre, bcat, M=RL, N=C, K=512, out=dkeys, b_mode=0, lda=512)
+        else:
+            self._dx(dKV, wkv, RL, dkeys, beta=1.0)
         self._dw_pe(dKV, s.keys2_b, RL, self._group(self.flat_grad, [f + "k_proj.weight", f + "v_proj.weight"], C),
-                    CI, s.pe_b, db=self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0))
+                    CI, s.pe_b, db=self._group(self.flat_grad, [f + "k_proj.bias", f + "v_proj.bias"], 0), ldy=lkv)
         # ---- two-way blocks in reverse
         for li in reversed(range(cfg.num_hidden_layers)):
             ls = s.layers[li]

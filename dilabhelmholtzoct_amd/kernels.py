@@ -375,10 +375,11 @@ def upmask_fwd(up1, w2, b2, hyper, P, ntok, masks):
     return masks
 
 
-def upmask_bwd(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper, ln=None):
+def upmask_bwd(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper, ln=None, ldd=256):
     """Backward of upmask_fwd: writes d up1 (bf16) and overwrites d w2, d b2, d hyper (fp32).
     ln = (x, mean, rstd, ln_w, ln_b, dln_w, dln_b): the LayerNorm2d + GELU that produced up1 from x is
-    differentiated in the same pass (octsam_upmask_ln_bwd); dup1 then receives d x, and dln_w / dln_b are overwritten."""
+    differentiated in the same pass (octsam_upmask_ln_bwd); dup1 then receives d x, and dln_w / dln_b are overwritten.
+    ldd (with ln): elements between the rows of d x's [P * 4096, 256] view (octsam_upmask_ln_bwd_strided)."""
     _require_cuda(up1, w2, b2, hyper, dmask, dup1, dw2, db2, dhyper)
     n = _lib.load().octsam_upmask_bwd_workspace(P, ntok)
     ws = torch.empty(n, device=up1.device, dtype=torch.float32)
@@ -388,6 +389,11 @@ def upmask_bwd(up1, w2, b2, hyper, dmask, P, ntok, dup1, dw2, db2, dhyper, ln=No
         return dup1
     x, mean, rstd, lw, lb, dlw, dlb = ln
     _require_cuda(x, mean, rstd, lw, lb, dlw, dlb)
+    if ldd != 256:
+        _lib.call("octsam_upmask_ln_bwd_strided", ptr(up1), ptr(w2), ptr(b2), ptr(hyper), ptr(dmask), P, ntok, ptr(x),
+                  ptr(mean), ptr(rstd), ptr(lw), ptr(lb), ptr(dup1), ldd, ptr(dw2), ptr(db2), ptr(dhyper), ptr(dlw),
+                  ptr(dlb), ptr(ws))
+        return dup1
     _lib.call("octsam_upmask_ln_bwd", ptr(up1), ptr(w2), ptr(b2), ptr(hyper), ptr(dmask), P, ntok, ptr(x), ptr(mean),
               ptr(rstd), ptr(lw), ptr(lb), ptr(dup1), ptr(dw2), ptr(db2), ptr(dhyper), ptr(dlw), ptr(dlb), ptr(ws))
     return dup1

@@ -327,6 +327,13 @@ int octsam_upmask_ln_bwd(const void* up1, const void* w2, const float* b2, const
                          int32_t P, int32_t ntok, const void* x, const float* mean, const float* rstd, const float* ln_w,
                          const float* ln_b, void* dx, float* dw2, float* db2, float* dhyper, float* dln_w, float* dln_b,
                          float* workspace, void* stream);
+/* octsam_upmask_ln_bwd with d x written at a row stride (row r of the [P * 4096, 256] view at dx + r * ldx, ldx >= 256,
+ * a multiple of 4), so d x can be the left half of a wider operand (ABI 20) */
+int octsam_upmask_ln_bwd_strided(const void* up1, const void* w2, const float* b2, const float* hyper,
+                                 const float* dmask, int32_t P, int32_t ntok, const void* x, const float* mean,
+                                 const float* rstd, const float* ln_w, const float* ln_b, void* dx, int64_t ldx,
+                                 float* dw2, float* db2, float* dhyper, float* dln_w, float* dln_b, float* workspace,
+                                 void* stream);
 
 /* ---------------------------------------------------------------- post-processing + losses
  * octsam_postproc_fwd: ref:octsam/models/training_utils.py:57-59 — lowres fp32 [M,S,S] -> bilinear to

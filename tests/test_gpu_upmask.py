@@ -116,3 +116,11 @@ def test_upmask_ln_bwd(cuda, P, ns):
     dx3, dlw3, dlb3 = torch.empty_like(x), torch.empty_like(dlw), torch.empty_like(dlb)
     kernels.upmask_bwd(up1, w2, b2, hyper, dmask, P, ns, dx3, dw2b, db2b, dhb, ln=(x, mean, rstd, lw, lb, dlw3, dlb3))
     assert torch.equal(dx, dx3) and torch.equal(dlw, dlw3) and torch.equal(dlb, dlb3)
+    # d x at a row stride (octsam_upmask_ln_bwd_strided: the left half of a [P * 4096, 512] operand), the right half
+    # untouched
+    wide = torch.full((P * 4096, 512), 7.0, device=cuda, dtype=torch.bfloat16)
+    dlw4, dlb4 = torch.empty_like(dlw), torch.empty_like(dlb)
+    kernels.upmask_bwd(up1, w2, b2, hyper, dmask, P, ns, wide, dw2b, db2b, dhb, ln=(x, mean, rstd, lw, lb, dlw4, dlb4),
+                       ldd=512)
+    assert torch.equal(wide[:, :256].reshape(P * 16384, 64), dx) and bool((wide[:, 256:] == 7.0).all())
+    assert torch.equal(dlw4, dlw) and torch.equal(dlb4, dlb)
