@@ -284,9 +284,11 @@ class MaskDecoder(nn.Module):
     # (token->image K / V: octsam_dec_t2i_bwd_sum; image->token Q: octsam_dec_i2t_bwd_sum; False: per-prompt gradients
     # + octsam_group_sum; A/B, scripts/step_ab3.py)
     t2i_sum = True
-    # the keys gradient of the mask head and the final attention as one product over [d up1pre | dK | dV] (False:
-    # two products, the second read-modify-writing d keys2; A/B, scripts/step_ab3.py)
-    fuse_dkeys = True
+    # the keys gradient of the mask head and the final attention as one product over [d up1pre | dK | dV] (True;
+    # False: two products, the second read-modify-writing d keys2). Off by default: 16.15 -> 16.09 ms per step, but its
+    # rounding moves the val-Dice protocol's warm state onto a trajectory where the fp32 oracle disagrees with ITSELF by
+    # up to 0.08 in Dice between processes (profiles/r04/valdice_chaos_dkeys.log); A/B: scripts/step_ab3.py
+    fuse_dkeys = False
     # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
     fused_ln_bwd = True
