@@ -2,7 +2,8 @@
 """Per-kernel HBM traffic table from two rocprofv3 PMC passes over the same command (FETCH_SIZE and
 WRITE_SIZE cannot share a pass on gfx950): bytes per launch, measured ÷ compulsory where the compulsory
 bytes of a kernel are known for the bench workload (B = 8 images, N = 21 prompts, vit-b), and the
-implied HBM rate over the launch's duration from the kernel trace of the fetch pass.
+implied HBM rate over the launch's duration from the kernel trace of the fetch pass. `--rescore <table.json>`
+recomputes a saved table's compulsory columns with the formulas below.
 
 FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled (gfx950 reports half the bytes of wide 16-B/lane
 streaming reads, MI355X_MICROARCH.md §HBM). Usage: pmc_kernels.py <dir with fetch/ write/> [out.json]"""
@@ -30,7 +31,17 @@ COMPULSORY = {
     # up1 bf16 [P * 16384, 64] (upmask.hip layout): forward reads it and writes the fp32 low-res masks; backward
     # reads up1 and d masks and writes d up1 (the W2 / b2 / hyper partials are small)
     "upmask_bwd_kernel": P * 16384 * 64 * 2 * 2 + P * 256 * 256 * 4,
+    # the form with the LayerNorm2d + GELU backward fused in (the step's default, upmask_bwd_kernel<1, true>): it also
+    # reads the ConvT1 output x (bf16, the up1 shape) and its per-row mean / rstd, and writes d x instead of d up1
+    "upmask_bwd_kernelILi1ELb1E": P * 16384 * 64 * 2 * 3 + P * 16384 * 4 * 2 + P * 256 * 256 * 4,
+    "upmask_bwd_kernel<1, true>": P * 16384 * 64 * 2 * 3 + P * 16384 * 4 * 2 + P * 256 * 256 * 4,
     "upmask_fwd_kernel": P * 16384 * 64 * 2 + P * 256 * 256 * 4,
+    # DiceCE backward fused with the row pass: masks fp32 + gt u8 in, row-pass tmp [P, 496, 256] fp32 out
+    "dicece_pp_rows_kernel": P * HW_OUT * 4 + P * HW_OUT + P * 496 * 256 * 4,
+    # first-block backwards with the prompt sums fused in: per-image K / V (resp. Q) rows in and gradients out once,
+    # per-prompt dO rows (i2t) in once, the fp32 dQ / dK-dV partials out
+    "t2i_bwd_sum_kernel": B * 4096 * 256 * 2 * 2 + P * (4096 // 64) * 4 * 256 * 4,
+    "i2t_bwd_sum_kernel": B * 4096 * 128 * 2 * 2 + P * 4096 * 128 * 2 + (4096 // 64) * P * 2 * 7 * 128 * 4,
 }
 
 
@@ -73,7 +84,25 @@ def short(k):
     return s.split("(")[0][:60]
 
 
+def rescore(path):
+    """Recompute the compulsory columns of a saved table (the measured bytes are kept) with this file's formulas."""
+    rows = json.load(open(path))
+    for row in rows:
+        row.pop("compulsory_MB", None)
+        row.pop("measured_over_compulsory", None)
+        for name, c in COMPULSORY.items():
+            if name in row["kernel"]:
+                row["compulsory_MB"] = round(c / MB, 2)
+                row["measured_over_compulsory"] = round(row["hbm_MB"] * MB / c, 3)
+    json.dump(rows, open(path, "w"), indent=1)
+    for r in rows[:40]:
+        print(json.dumps(r))
+
+
 def main():
+    if sys.argv[1] == "--rescore":  # pmc_kernels.py --rescore <table.json> (prints the text table)
+        rescore(sys.argv[2])
+        return
     d = sys.argv[1]
     fetch, write, dur = load(os.path.join(d, "fetch"), "FETCH_SIZE"), load(os.path.join(d, "write"), "WRITE_SIZE"), \
         durations(os.path.join(d, "fetch"))
