@@ -38,8 +38,8 @@ def main():
                 "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
                 "g4res_off": ({}, {}), "attn_v2": ({}, {}), "pp_unfused": ({"fused_pp": False}, {}),
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
-                "dkeys_joint": ({}, {"fuse_dkeys": True})}
-    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24}
+                "dkeys_joint": ({}, {"fuse_dkeys": True}), "g4w_off": ({}, {})}
+    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
