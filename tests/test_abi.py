@@ -54,3 +54,27 @@ def test_gemm_rejects_bad_arguments_without_launching():
     rc = lib.octsam_gemm(a, None)
     assert rc != 0
     assert lib.octsam_last_error()
+
+
+def test_round4_entries_reject_bad_arguments_without_launching():
+    """The round-4 entry points validate on the host before any launch (no GPU needed): null operands, a chunk
+    length that does not divide L, a row stride below the row width each fail with a message."""
+    lib = _lib.load()
+    fake = 1 << 20  # a non-null, 16-B aligned address that is never dereferenced (validation fails first)
+    # t2i / i2t backwards with the prompt sum fused in: L % 64 != 0
+    rc = lib.octsam_dec_t2i_bwd_sum(fake, fake, fake, 384, 3, 6, 7, 4000, fake, fake, fake, fake, fake, fake, 256,
+                                    fake, None)
+    assert rc != 0 and b"t2i_bwd_sum" in lib.octsam_last_error()
+    rc = lib.octsam_dec_i2t_bwd_sum(fake, 384, 3, fake, fake, 6, 7, 4000, fake, 128, fake, 128, fake, None)
+    assert rc != 0 and b"i2t_bwd_sum" in lib.octsam_last_error()
+    # the strided mask-head backward: a row stride below 256
+    rc = lib.octsam_upmask_ln_bwd_strided(fake, fake, fake, fake, fake, 4, 1, fake, fake, fake, fake, fake, fake, 128,
+                                          fake, fake, fake, fake, fake, fake, None)
+    assert rc != 0 and b"strided" in lib.octsam_last_error()
+    # null operand
+    rc = lib.octsam_dec_t2i_bwd_sum(None, fake, fake, 384, 3, 6, 7, 4096, fake, fake, fake, fake, fake, fake, 256,
+                                    fake, None)
+    assert rc != 0
+    # sizes of the workspaces / partials the entries expect
+    assert lib.octsam_dec_t2i_bwd_sum_workspace(168, 7, 4096) == 168 * 64 * 4 * 256 + 168 * 8 * 7 * 2
+    assert lib.octsam_dec_i2t_bwd_sum_partials(168, 7, 4096) == 64 * 168 * 2 * 7 * 128
