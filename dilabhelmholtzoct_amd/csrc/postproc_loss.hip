@@ -414,8 +414,23 @@ __global__ __launch_bounds__(256) void pp_bwd_cols_kernel(const float* __restric
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= S * S) return;
   const int a = e / S, b = e % S;
+  const int k0 = rptr[a], k1 = rptr[a + 1];
+  const float* src = tmp + (long long)m * oh * S + b;
+  // the first CT taps' loads issued together (a row's taps: about 8 at the step's 256 -> 1024 -> 496 resampling), then
+  // summed in tap order as the plain loop does (bit-identical); any further taps by the plain loop
+  constexpr int CT = 12;
+  float v[CT], wv[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const bool on = k0 + t < k1;
+    wv[t] = on ? rw[k0 + t] : 0.0f;
+    v[t] = on ? src[(long long)ridx[k0 + t] * S] : 0.0f;
+  }
   float acc = 0.0f;
-  for (int k = rptr[a]; k < rptr[a + 1]; ++k) acc += rw[k] * tmp[((long long)m * oh + ridx[k]) * S + b];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+    if (k0 + t < k1) acc += wv[t] * v[t];
+  for (int k = k0 + CT; k < k1; ++k) acc += rw[k] * src[(long long)ridx[k] * S];
   dlow[(long long)m * S * S + e] = acc;
 }
 
