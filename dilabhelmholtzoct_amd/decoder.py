@@ -353,7 +353,8 @@ class MaskDecoder(nn.Module):
             Ks = M // split
         dev = out.device
         if db is not None and M < 65536:  # (the small-problem tile kernel has no fused column sums)
-            K.colsum(dy if ldy == O else dy.view(M, ldy)[:, :O].contiguous(), M, O, db)
+            # (dy may be a column slice of a wider buffer, e.g. dKV_img[:, CI:] at ldy = 2*CI: address it by stride)
+            K.colsum(dy if ldy == O else torch.as_strided(dy, (M, O), (ldy, 1)).contiguous(), M, O, db)
             db = None
         pa = torch.empty((split, O), device=dev, dtype=torch.float32) if db is not None else None
         pb = torch.empty((split, I), device=dev, dtype=torch.float32) if dbx is not None else None

@@ -160,6 +160,15 @@ def _keep_table(B: int, N: int, maps, device):
     return _KEEP[key]
 
 
+def dicece_pp_rows_supported(B: int, N: int, H: int, W: int) -> bool:
+    """Whether octsam_dicece_pp_rows (and octsam_pp_bwd_rows_maps) take a [B, N, H, W] batch: at most 32 prompts whose
+    rows fit 160 KB of LDS, W % 4 == 0, W <= 1024. The reference puts no cap on the prompt count (one prompt per
+    8-connected component of every label value, training_utils.py:389-415), so callers fall back to
+    dicece_forward_backward + postproc_backward when this is False."""
+    return (0 < N <= 32 and N * W * 4 <= 160 * 1024 and W % 4 == 0 and 0 < W <= 1024 and B * H * W < (1 << 31)
+            and B <= 65535)
+
+
 def dicece_pp_rows(masks: torch.Tensor, gt_u8: torch.Tensor, dice_part: torch.Tensor, crop, *, maps=(),
                    w_dice: float = 1.0, w_ce: float = 1.0, S: int = 256):
     """The DiceCE loss and its backward fused with the post-processing adjoint's row pass (octsam_dicece_pp_rows):

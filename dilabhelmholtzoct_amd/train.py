@@ -21,8 +21,8 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .losses import (dicece_forward_backward, dicece_pp_rows, postproc_backward, postproc_forward, pp_rows_finish,
-                     topo_device_backward, topo_device_forward, topo_host, topo_index, topo_w2_device)
+from .losses import (dicece_forward_backward, dicece_pp_rows, dicece_pp_rows_supported, postproc_backward,
+                     postproc_forward, pp_rows_finish, topo_device_backward, topo_device_forward, topo_host, topo_index, topo_w2_device)
 from .model import SamModel
 
 
@@ -178,7 +178,10 @@ class FusedTrainStep:
         """DiceCE loss + backward. fused_pp (default): fused with the post-processing adjoint's row pass, the
         topological loss's maps kept as d-masks for B (losses.dicece_pp_rows); else the [B, N, H, W] d-mask."""
         B, N, H, W = st.masks.shape
-        if self.fused_pp:
+        # the fused kernel takes at most 32 prompts and W % 4 == 0; other batches (the reference caps neither) take
+        # the two-kernel path, chosen per batch shape (so per captured graph set)
+        st.fused_pp = self.fused_pp and dicece_pp_rows_supported(B, N, H, W)
+        if st.fused_pp:
             maps = st.topo_dev[1] if st.topo_dev is not None else ()
             st.loss3, st.pp_tmp, st.dkeep = dicece_pp_rows(st.masks, st.gt_u8.view(B, N, H, W), st.dpart, st.crop,
                                                            maps=maps)
@@ -211,11 +214,11 @@ class FusedTrainStep:
             if st.topo_dev is not None:
                 if self.w2 == "host" and st.pinned is not None:
                     st.dp.copy_(st.dp_pinned, non_blocking=True)
-                if self.fused_pp:
+                if st.fused_pp:
                     topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dkeep, interp=self.interp, compact=True)
                 else:
                     topo_device_backward(st.masks, st.topo_dev[2], st.dp, st.dmask, interp=self.interp)
-            if self.fused_pp:
+            if st.fused_pp:
                 dlow = pp_rows_finish(st.pp_tmp, st.crop, st.orig, dkeep=st.dkeep,
                                       midx=st.topo_dev[2] if st.topo_dev is not None else None)
             else:

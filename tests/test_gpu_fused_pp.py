@@ -18,7 +18,8 @@ def _case(cuda, B, N, seed, crop=(1024, 993), orig=(496, 512)):
     return masks.view(B, N, *orig), gt.view(B, N, *orig), part, crop, orig
 
 
-@pytest.mark.parametrize("B,N,maps", [(2, 5, ()), (2, 5, (0, 5)), (1, 21, (0,)), (3, 1, (0, 1, 2))])
+@pytest.mark.parametrize("B,N,maps", [(2, 5, ()), (2, 5, (0, 5)), (1, 21, (0,)), (3, 1, (0, 1, 2)),
+                                     (1, 28, (0,)), (2, 32, (0, 32))])
 def test_fused_pp_matches_two_kernel_path(cuda, B, N, maps):
     from dilabhelmholtzoct_amd.losses import (dicece_forward_backward, dicece_pp_rows, postproc_backward,
                                               pp_rows_finish, topo_device_backward)
@@ -68,3 +69,38 @@ def test_train_step_fused_pp_matches_unfused(cuda):
     for a, b in zip(la, lb):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-9), (a, b)
     assert (fa - fb).abs().max().item() <= 1e-5 * fa.abs().max().item()
+
+
+def _wide_batch(cuda, reps):
+    """A real two-image batch whose prompt dimension is repeated `reps` times (N = 21 * reps > 32 for reps >= 2):
+    more components than the fused DiceCE / row-pass kernel takes (the reference caps neither)."""
+    from dilabhelmholtzoct_amd import data
+    sd = data.SAMDataset(data.synthetic_oct(seed=3, n=2), {"prompt_type": "bboxes"}, epoch_seed=0)
+    b = data.process_batch(data.make_processor(), data.custom_collate([sd[0], sd[1]]), "bboxes")
+    for k in ("input_boxes", "gt_u8", "mask_values"):
+        b[k] = torch.cat([b[k]] * reps, 1)
+    return data.to_device_batch(b, cuda)
+
+
+def test_train_step_over_32_prompts_falls_back(cuda):
+    """N > 32 prompts: FusedTrainStep (fused_pp on by default) takes the two-kernel DiceCE + post-processing backward
+    instead of raising in octsam_dicece_pp_rows, so its steps equal those with fused_pp off bit for bit."""
+    from dilabhelmholtzoct_amd.losses import dicece_pp_rows_supported
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep
+    batch = _wide_batch(cuda, 2)
+    B, N = batch["gt_u8"].shape[:2]
+    assert N > 32 and not dicece_pp_rows_supported(B, N, *batch["gt_u8"].shape[2:])
+    runs = []
+    for fused in (True, False):
+        model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(cuda)
+        step = FusedTrainStep(model, topological=True, graphs=True)
+        step.fused_pp = fused
+        losses = [step.step(batch).clone() for _ in range(2)]
+        step.flush()
+        torch.cuda.synchronize()
+        runs.append((losses, model.mask_decoder.flat.detach().clone()))
+    (la, fa), (lb, fb) = runs
+    for a, b in zip(la, lb):
+        assert torch.isfinite(a).all() and torch.equal(a, b), (a, b)
+    assert torch.equal(fa, fb)

@@ -95,3 +95,15 @@ def test_topo_entries(B, N, mode):
         assert len(ent) == N
     elif N == 1 or mode == "first":
         assert len(ent) == B
+
+
+def test_dicece_pp_rows_supported_limits():
+    """The fused DiceCE / row-pass kernel's limits as the host checks them before choosing it (train._dicece falls back
+    to the two-kernel path outside them): N <= 32 prompts, W % 4 == 0, W <= 1024."""
+    from dilabhelmholtzoct_amd.losses import dicece_pp_rows_supported
+    assert dicece_pp_rows_supported(8, 21, 496, 512)
+    assert dicece_pp_rows_supported(8, 32, 496, 512)
+    assert not dicece_pp_rows_supported(8, 33, 496, 512)
+    assert not dicece_pp_rows_supported(8, 21, 496, 510)
+    assert not dicece_pp_rows_supported(1, 2, 100, 2048)
+    assert not dicece_pp_rows_supported(8, 0, 496, 512)
