@@ -422,21 +422,21 @@ def top_off_leg(args, model, batch, steps=10):
 
 
 def val_protocol(args, device):
-    """The val-Dice half of the metric on SURVEY.md §8(d)'s protocol, HIP side of tests/test_gpu_val_dice.py
-    (ref:octsam/models/training_utils.py:113-156, 246): the synthetic vit-b weights (seed 0) with the committed start
-    decoder, 64 warm steps on its own synthetic set, then 4 epochs (64 steps) on the test's 128 scans, the held-out
-    32 scans scored after every epoch, beside the fp32 oracle's values from the same protocol
-    (tests/golden/valdice_oracle.json, made by the test on MI355X). Batches come from the HIP data path (bit-identical
-    to the host SAMDataset + collate + SamProcessor path the test uses: test_gpu_training_loop.py); the step is the
-    benchmarked one (hipGraphs + encoder lookahead)."""
-    from safetensors.torch import load_file
+    """The val-Dice half of the metric on the multi-seed protocol of tests/valdice_protocol.py (SURVEY.md §8(d);
+    ref:octsam/models/training_utils.py:113-156, 246), HIP side of tests/test_gpu_val_dice.py: the synthetic vit-b
+    weights (seed 0) with the ORACLE-made warm start (tests/golden/valdice_warm_oracle.safetensors: decoder + Adam
+    state), then per (training, held-out) seed pair 4 epochs (64 steps) on 128 scans, the 32 held-out scans scored
+    after every epoch, beside the fp32 oracle's values from the same start (tests/golden/valdice_oracle.json, made by
+    tests/golden/make_valdice_golden.py on MI355X with the oracle alone, so they hold for any HIP build). Batches come
+    from the HIP data path (bit-identical to the host SAMDataset + collate + SamProcessor path the test uses:
+    test_gpu_training_loop.py); the step is the benchmarked one (hipGraphs + encoder lookahead)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import valdice_protocol as P
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.components import collate_device
-    from dilabhelmholtzoct_amd.model import SamModel
     from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
-    from dilabhelmholtzoct_amd.train import FusedTrainStep, class_confusion, mean_dice, predict_masks
-    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "valdice_oracle.json")))
-    name, bs, lr = "facebook/sam-vit-base", 8, 1e-3
+    gold = json.load(open(P.ORACLE_JSON))
+    gold_pairs = {(g["train_seed"], g["val_seed"]): g for g in gold["pairs"]}
     t0 = time.perf_counter()
     dproc = DeviceProcessor(device)
     raw = {}
@@ -447,65 +447,32 @@ def val_protocol(args, device):
             raw[seed] = (np.stack([np.array(d["image"]) for d in ds]), np.stack([np.array(d["label"]) for d in ds]))
         imgs, labs = raw[seed]
         out = []
-        for s in range(0, n, bs):
-            e = min(n, s + bs)
+        for s in range(0, n, P.BS):
+            e = min(n, s + P.BS)
             hooks = [(lambda i=i: data.seed_sample(epoch, i, seed)) for i in range(s, e)]
             b = collate_device(imgs[s:e], labs[s:e], "bboxes", device, seed_hooks=hooks, processor=dproc)
             b.pop("prompt_raw", None)
             out.append(b)
         return out
 
-    model = SamModel(name)
-    model.init_weights(seed=0)
-    start = {k: v.float() for k, v in load_file(os.path.join(ROOT, "tests", "golden",
-                                                              "valdice_start_decoder.safetensors")).items()}
-    missing = set(start) - set(model.state_dict())
-    if missing:
-        raise RuntimeError(f"start decoder keys not in the model: {sorted(missing)[:3]}")
-    model.load_state_dict(start, strict=False)
-    model = model.to(device)
-    step = FusedTrainStep(model, lr=lr, topological=True, graphs=True, pipeline=True)
-
-    def run(seed, epochs, limit=None, evals=None):
-        k = 0
-        for ep in range(epochs):
-            tr = epoch_batches(seed, 128, ep)
-            for i, b in enumerate(tr):
-                if limit is not None and k >= limit:
-                    return
-                last = i + 1 == len(tr) or (limit is not None and k + 1 >= limit)
-                step.step(b, next_batch=None if last else tr[i + 1])
-                k += 1
-            if evals is not None:
-                evals.append(dice())
-
-    val = epoch_batches(3001, 32, 0)
-
-    def dice():
-        step.flush()
-        c = torch.zeros(14, 3, dtype=torch.int64)
-        for v in val:
-            c += class_confusion(predict_masks(model, v), v["gt_u8"], v["mask_values"])
-        return round(mean_dice(c), 5)
-
-    run(2000, 4, limit=64)
-    hip = [dice()]
-    # the warm state the committed oracle values start from (tests/test_gpu_val_dice.py warm_fingerprint)
-    wsd = {n: t.detach().float().cpu() for n, t in model.mask_decoder.state_dict().items()}
-    fp = [round(sum(float(t.double().sum()) for t in wsd.values()), 6),
-          round(sum(float((t.double() ** 2).sum()) for t in wsd.values()), 6)]
-    del wsd
-    run(2001, 4, evals=hip)
-    ora = gold["oracle_dice"]
-    diffs = [round(h - o, 5) for h, o in zip(hip, ora)]
-    out = {"steps": gold["steps"], "hip": hip, "oracle": ora, "diff": diffs,
-           "max_abs_diff": round(max(abs(d) for d in diffs), 5), "tolerance": 0.005,
-           "within": bool(max(abs(d) for d in diffs) <= 0.005), "seconds": round(time.perf_counter() - t0, 1),
-           "warm_fingerprint": fp, "warm_state_matches_golden": fp == gold.get("warm_fingerprint"),
-           "protocol": "tests/test_gpu_val_dice.py (warm start: 64 HIP steps; 4 epochs x 16 steps; 32 held-out scans)",
+    state, adam = P.load_warm()
+    pairs = []
+    for tr, va in P.SEEDS:
+        hip = [round(P.dice_of(c), 5) for _, c in P.hip_run(device, state, adam, tr, va, epoch_batches=epoch_batches,
+                                                               val_batches=epoch_batches(va, P.N_VAL, 0))]
+        g = gold_pairs[(tr, va)]
+        pairs.append({"train_seed": tr, "val_seed": va, "hip": hip, "oracle": g["oracle_dice"],
+                      "diff": [round(h - o, 5) for h, o in zip(hip, g["oracle_dice"])],
+                      "oracle_spread": g["spread"]})
+    n = len(pairs)
+    mean_diff = [round(sum(p["diff"][i] for p in pairs) / n, 5) for i in range(len(P.CHECKPOINTS))]
+    out = {"steps": P.CHECKPOINTS, "pairs": pairs, "mean_diff": mean_diff,
+           "max_abs_mean_diff": round(max(abs(d) for d in mean_diff), 5), "tolerance": P.TOL,
+           "within": bool(max(abs(d) for d in mean_diff) <= P.TOL), "seconds": round(time.perf_counter() - t0, 1),
+           "protocol": "tests/valdice_protocol.py (oracle-made warm start; per seed pair 4 epochs x 16 steps; 32 "
+                       "held-out scans; mean over pairs of Dice_HIP - Dice_oracle)",
            "oracle_source": "tests/golden/valdice_oracle.json"}
-    log(f"val protocol: {out}")
-    del step, model
+    log(f"val protocol: mean diff {mean_diff} ({out['seconds']} s)")
     torch.cuda.empty_cache()
     return out
 

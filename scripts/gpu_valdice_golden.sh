@@ -1,9 +1,16 @@
 #!/bin/bash
-# Regenerates the oracle side of the val-Dice protocol (tests/golden/valdice_oracle.json) after a change to the HIP
-# step's numerics: the protocol's warm start is 64 HIP steps, so the oracle's trajectory starts from the HIP code's
-# own warm state. Runs tests/test_gpu_val_dice.py (which asserts every epoch within +-0.005) and writes its values.
+# Makes the val-Dice protocol's fixtures with the fp32 oracle alone (tests/golden/make_valdice_golden.py): the
+# oracle-made warm start (--warm) and the per-seed-pair oracle values + perturbation spread (--oracle), into
+# gpurun_out/$TAG (copied into tests/golden/ by hand after the run). Depends on no HIP kernel, so it runs once.
 set -u
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-valdice}; mkdir -p $O; cd $R
-OCTSAM_VALDICE_OUT=$O/valdice_oracle_run.json timeout -k 10 900 python -u -m pytest -x -v -s --timeout 800 --timeout-method thread tests/test_gpu_val_dice.py > $O/pytest_valdice.log 2>&1 || { tail -30 $O/pytest_valdice.log; exit 1; }
-grep -E "after|fingerprint|passed|failed" $O/pytest_valdice.log
-cat $O/valdice_oracle_run.json
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-valdice_golden}; mkdir -p $O; cd $R
+STEP=${STEP:-both}
+if [ "$STEP" = warm ] || [ "$STEP" = both ]; then
+  timeout -k 10 600 python -u tests/golden/make_valdice_golden.py --warm --warm-out $O/valdice_warm_oracle.safetensors > $O/warm.log 2>&1 || { tail -20 $O/warm.log; exit 1; }
+  tail -2 $O/warm.log
+  cp $O/valdice_warm_oracle.safetensors tests/golden/valdice_warm_oracle.safetensors
+fi
+if [ "$STEP" = oracle ] || [ "$STEP" = both ]; then
+  timeout -k 10 1000 python -u tests/golden/make_valdice_golden.py --oracle --oracle-out $O/valdice_oracle.json > $O/oracle.log 2>&1 || { tail -20 $O/oracle.log; exit 1; }
+  tail -4 $O/oracle.log
+fi

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Makes the val-Dice protocol's committed fixtures (tests/valdice_protocol.py) with the fp32 ORACLE only, on an
+MI355X (the oracle's SamModel runs on the GPU to keep this short; oracle_mode makes it run-to-run reproducible):
+
+  --warm    tests/golden/valdice_warm_oracle.safetensors: the committed start decoder continued by the oracle for
+            WARM_STEPS steps (cold Adam) on synthetic_oct(seed=2000); decoder weights and Adam moments rounded to bf16
+            for storage, the step count as fp32. This file is the protocol's start state on both sides.
+  --oracle  tests/golden/valdice_oracle.json: for every (training, held-out) seed pair the oracle's held-out Dice at
+            every checkpoint from that start state, plus the oracle's own spread per checkpoint (the same run from
+            N_PERTURB copies of the start with each decoder weight times 1 + 2^-8 u): the protocol's noise floor.
+
+Test infrastructure: imports oracle/ (and nothing of it reaches the product path)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402
+
+import valdice_protocol as P  # noqa: E402
+
+N_PERTURB = 2
+
+
+def make_warm(cuda, out):
+    from safetensors.torch import load_file, save_file
+    state = P.base_state()
+    for k, v in load_file(P.START).items():
+        assert k in state and state[k].shape == v.shape, k
+        state[k] = v.float()
+    runner = P.OracleRunner(cuda)
+    ref = runner.make(state)
+    k, ep = 0, 0
+    while k < P.WARM_STEPS:
+        k += runner.train_steps(ref, P.WARM_SEED, ep, limit=P.WARM_STEPS - k)
+        ep += 1
+    d = P.dice_of(runner.conf(ref, P.WARM_VAL_SEED))
+    sd = {"mask_decoder." + n: t.detach().to(torch.bfloat16).cpu().contiguous()
+          for n, t in ref.model.mask_decoder.state_dict().items()}
+    step = None
+    for name, p in ref.model.mask_decoder.named_parameters():
+        st = ref.opt.state.get(p, {})
+        if "step" in st:
+            step = float(st["step"])
+        for key in ("exp_avg", "exp_avg_sq"):
+            t = st[key] if st else torch.zeros_like(p)
+            sd[f"{key}.mask_decoder.{name}"] = t.detach().to(torch.bfloat16).cpu().contiguous()
+    sd["step"] = torch.tensor([step], dtype=torch.float32)
+    save_file(sd, out)
+    print(json.dumps({"warm": out, "steps": k, "epochs_started": ep, "adam_step": step,
+                      "val_dice_seed3000": round(d, 5)}), flush=True)
+
+
+def make_oracle(cuda, out):
+    from oracle.eval_ref import mean_specificity_ref
+    state, adam = P.load_warm()
+    runner = P.OracleRunner(cuda)
+    pairs = []
+    t0 = time.time()
+    for tr, va in P.SEEDS:
+        base, moved = runner.run(state, adam, tr, va)
+        rec = {"train_seed": tr, "val_seed": va, "steps": [k for k, _ in base],
+               "oracle_dice": [round(P.dice_of(c), 5) for _, c in base],
+               "oracle_specificity": round(mean_specificity_ref(base[-1][1]), 4), "oracle_moved": round(moved, 4)}
+        spread = []
+        for j in range(N_PERTURB):
+            pert, _ = runner.run(P.perturbed(state, 100 + j), adam, tr, va)
+            spread.append([round(P.dice_of(c), 5) for _, c in pert])
+        rec["perturbed_dice"] = spread
+        rec["spread"] = [round(max([b] + [s[i] for s in spread]) - min([b] + [s[i] for s in spread]), 5)
+                         for i, b in enumerate(rec["oracle_dice"])]
+        pairs.append(rec)
+        print(json.dumps(rec), flush=True)
+    n = len(pairs)
+    mean = [round(sum(p["oracle_dice"][i] for p in pairs) / n, 5) for i in range(len(P.CHECKPOINTS))]
+    doc = {"protocol": "tests/valdice_protocol.py: sam-vit-base synthetic weights (seed 0); start state "
+                       "tests/golden/valdice_warm_oracle.safetensors (the fp32 oracle: the committed start decoder + "
+                       f"{P.WARM_STEPS} oracle steps on synthetic_oct(seed={P.WARM_SEED}), bf16-stored); per seed "
+                       f"pair {P.EPOCHS} epochs on synthetic_oct(train seed, n={P.N_TRAIN}), B={P.BS}, box prompts, "
+                       f"--top=True, lr {P.LR}; held-out synthetic_oct(val seed, n={P.N_VAL}), epoch-0 prompts; mean "
+                       "per-class Dice after every epoch",
+           "made_by": "tests/golden/make_valdice_golden.py --oracle on MI355X (oracle/step_ref.py in oracle_mode: "
+                      "MIOpen off, torch deterministic algorithms); depends on no HIP kernel",
+           "steps": P.CHECKPOINTS, "pairs": pairs, "oracle_mean_dice": mean,
+           "noise_floor": f"per pair, spread = max - min of the oracle's Dice over the base run and {N_PERTURB} runs "
+                          "from the start state with every decoder weight times (1 + 2^-8 u), u ~ U(-1, 1)",
+           "seconds": round(time.time() - t0, 1)}
+    with open(out, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps({"oracle_mean_dice": mean}), flush=True)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--warm", action="store_true")
+    p.add_argument("--oracle", action="store_true")
+    p.add_argument("--warm-out", default=P.WARM)
+    p.add_argument("--oracle-out", default=P.ORACLE_JSON)
+    a = p.parse_args()
+    cuda = torch.device("cuda", 0)
+    if a.warm:
+        make_warm(cuda, a.warm_out)
+    if a.oracle:
+        make_oracle(cuda, a.oracle_out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+"""The val-Dice protocol (BASELINE.json north_star: "val Dice within ±0.005 of the CPU reference on identical seeds";
+SURVEY.md §8(d)) shared by tests/test_gpu_val_dice.py, tests/golden/make_valdice_golden.py and bench.py.
+
+Protocol (ref:octsam/models/training_utils.py:27-80 training, :113-156 the pooled evaluation, :246 its mean Dice):
+sam-vit-base with the synthetic encoder / prompt-encoder weights (seed 0), box prompts, --top=True, lr 1e-3 (the
+reference CLI's default), B = 8, the reference's prompt redraw every epoch (SAMDataset.__getitem__).
+
+* Warm start, made by the ORACLE: the committed start decoder (tests/golden/valdice_start_decoder.safetensors, the
+  fp32 oracle after 256 steps on another synthetic set, past the all-foreground transition every random start goes
+  through) continued by the fp32 oracle for WARM_STEPS steps on synthetic_oct(seed=2000) with a cold Adam, stored
+  as tests/golden/valdice_warm_oracle.safetensors (decoder weights and Adam moments rounded to bf16 for storage,
+  the step count). That file IS the start state: both sides load it, so the compared trajectories start identical
+  and the committed oracle values never depend on HIP numerics (round 4's warm start was 64 HIP steps, so its
+  oracle column had to be regenerated whenever a HIP kernel's rounding changed).
+* For each (training seed, held-out seed) pair of SEEDS: EPOCHS epochs on 128 synthetic scans of the training seed,
+  the 32 held-out scans of the held-out seed scored after every epoch (CHECKPOINTS steps).
+* Compared: the MEAN over the seed pairs of Dice_HIP - Dice_oracle at every checkpoint, against TOL. One chaotic
+  trajectory cannot tell a kernel bias from the protocol's own noise (the oracle's spread under bf16-sized weight
+  perturbations reaches 0.008 at steps 56-64 on one seed, profiles/r04/valdice_spread_warm.jsonl); the mean over
+  independent seed pairs can. tests/golden/valdice_oracle.json carries each pair's oracle values and the oracle's own
+  perturbation spread per checkpoint.
+
+The HIP half imports only the product package; everything that touches oracle/ imports it inside the function, so
+bench.py (which may not use the oracle outside its cpu_baseline leg) can share this file."""
+from __future__ import annotations
+
+import contextlib
+import os
+
+import torch
+
+NAME = "facebook/sam-vit-base"
+LR = 1e-3
+BS = 8
+EPOCHS = 4
+N_TRAIN, N_VAL = 128, 32
+WARM_STEPS, WARM_SEED, WARM_VAL_SEED = 64, 2000, 3000
+SEEDS = [(2001, 3001), (2002, 3002), (2003, 3003)]
+CHECKPOINTS = [0] + [(N_TRAIN // BS) * (e + 1) for e in range(EPOCHS)]
+TOL = 0.005
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+START = os.path.join(GOLDEN, "valdice_start_decoder.safetensors")
+WARM = os.path.join(GOLDEN, "valdice_warm_oracle.safetensors")
+ORACLE_JSON = os.path.join(GOLDEN, "valdice_oracle.json")
+
+
+def host_batches(seed: int, n: int, epoch: int):
+    """One epoch of CPU batches through the reference's host path (SAMDataset + custom_collate + SamProcessor)."""
+    from dilabhelmholtzoct_amd import data
+    proc = data.make_processor()
+    sd = data.SAMDataset(data.synthetic_oct(seed=seed, n=n), {"prompt_type": "bboxes"}, epoch_seed=seed)
+    sd.epoch = epoch
+    return [data.process_batch(proc, data.custom_collate([sd[i] for i in range(s, min(n, s + BS))]), "bboxes")
+            for s in range(0, n, BS)]
+
+
+@contextlib.contextmanager
+def oracle_mode():
+    """The oracle's torch ops, run-to-run reproducible: MIOpen off (its solution choice for the decoder's
+    ConvTranspose2d depends on what ran before in the process) and torch's deterministic algorithms."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        with torch.backends.cudnn.flags(enabled=False):
+            yield
+    finally:
+        torch.use_deterministic_algorithms(prev)
+
+
+def base_state() -> dict:
+    """The synthetic sam-vit-base weights (seed 0) on the CPU: the encoder / prompt encoder of both sides."""
+    from dilabhelmholtzoct_amd.model import SamModel
+    m = SamModel(NAME)
+    m.init_weights(seed=0)
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def load_warm(path: str = WARM):
+    """-> (full fp32 state dict: synthetic encoder + the warm decoder, Adam state by HF name as
+    FusedTrainStep.optimizer_state() lays it out)."""
+    from safetensors.torch import load_file
+    raw = load_file(path)
+    state = base_state()
+    for k, v in raw.items():
+        if k.startswith("mask_decoder."):
+            if k not in state or tuple(state[k].shape) != tuple(v.shape):
+                raise ValueError(f"warm-state tensor {k} does not match the model")
+            state[k] = v.float()
+    adam = {k: v.float() for k, v in raw.items() if k.startswith("exp_avg")}
+    adam["step"] = raw["step"].float().reshape(())
+    return state, adam
+
+
+def perturbed(state: dict, seed: int) -> dict:
+    """The decoder weights each times (1 + 2^-8 u), u ~ U(-1, 1): bf16-rounding-sized noise (the oracle's own
+    spread along the protocol)."""
+    g = torch.Generator().manual_seed(seed)
+    out = dict(state)
+    for k, v in state.items():
+        if k.startswith("mask_decoder."):
+            out[k] = v * (1 + 2.0 ** -8 * (2 * torch.rand(v.shape, generator=g) - 1))
+    return out
+
+
+def dice_of(conf) -> float:
+    """Mean per-class Dice of pooled (tp, fp, fn[, tn]) counts [14, >=3] (training_utils.py:156, :246)."""
+    d = []
+    for tp, fp, fn in conf[:, :3].tolist():
+        den = 2 * tp + fp + fn
+        d.append(2 * tp / den if den else 0.0)
+    return sum(d) / len(d)
+
+
+def hip_run(cuda, state, adam, train_seed, val_seed, *, epoch_batches=None, val_batches=None):
+    """The HIP side exactly as bench.py runs it (FusedTrainStep, hipGraphs + the encoder lookahead) from the warm
+    state -> [(step, confusion [14, 3])] at CHECKPOINTS. epoch_batches(seed, n, epoch) / val_batches: device batch
+    factories (default: the host path moved to the device)."""
+    from dilabhelmholtzoct_amd import data
+    from dilabhelmholtzoct_amd.model import SamModel
+    from dilabhelmholtzoct_amd.train import FusedTrainStep, class_confusion, predict_masks
+    if epoch_batches is None:
+        def epoch_batches(seed, n, epoch):
+            return [data.to_device_batch(b, cuda) for b in host_batches(seed, n, epoch)]
+    val = val_batches if val_batches is not None else epoch_batches(val_seed, N_VAL, 0)
+    model = SamModel(NAME)
+    model.load_state_dict(state)
+    model = model.to(cuda)
+    step = FusedTrainStep(model, lr=LR, topological=True, graphs=True, pipeline=True)
+    step.load_optimizer_state(adam)
+
+    def conf():
+        step.flush()
+        c = torch.zeros(14, 3, dtype=torch.int64)
+        for v in val:
+            c += class_confusion(predict_masks(model, v), v["gt_u8"], v["mask_values"])
+        return c
+
+    out = [(0, conf())]
+    k = 0
+    for ep in range(EPOCHS):
+        tr = epoch_batches(train_seed, N_TRAIN, ep)
+        for i, b in enumerate(tr):
+            step.step(b, next_batch=tr[i + 1] if i + 1 < len(tr) else None)
+            k += 1
+        out.append((k, conf()))
+    del step, model
+    torch.cuda.empty_cache()
+    return out
+
+
+class OracleRunner:
+    """The fp32 oracle side (oracle/step_ref.py: transformers SamModel fp32 -- on the GPU only to keep the test
+    short -- restated DiceCE / topo loss, torch Adam; scored by oracle/eval_ref.pooled_confusion_ref, the reference's
+    threshold and break quirk). The frozen encoder's embeddings are cached per (seed, batch index)."""
+
+    def __init__(self, cuda):
+        self.cuda = cuda
+        self._emb = {}
+        self._val = {}
+
+    def _embedding(self, ref, key, batch):
+        if key not in self._emb:
+            with oracle_mode():
+                self._emb[key] = ref.embed(batch)
+        return self._emb[key]
+
+    def make(self, state, adam=None):
+        from oracle.step_ref import CpuReferenceStep
+        with oracle_mode():
+            ref = CpuReferenceStep(NAME, topological=True, lr=LR, state_dict=state, device=self.cuda,
+                                   loss_device=self.cuda)
+        if adam is not None:
+            for name, p in ref.model.mask_decoder.named_parameters():
+                m, v = adam[f"exp_avg.mask_decoder.{name}"], adam[f"exp_avg_sq.mask_decoder.{name}"]
+                if not bool(v.any()):  # (parameters that never had a gradient keep no state in torch)
+                    continue
+                ref.opt.state[p] = {"step": torch.tensor(float(adam["step"])), "exp_avg": m.to(p.device).clone(),
+                                    "exp_avg_sq": v.to(p.device).clone()}
+        return ref
+
+    def conf(self, ref, val_seed):
+        from oracle.eval_ref import pooled_confusion_ref
+        if val_seed not in self._val:
+            self._val[val_seed] = host_batches(val_seed, N_VAL, 0)
+        c = torch.zeros(14, 4, dtype=torch.int64)
+        with torch.no_grad(), oracle_mode():
+            for i, v in enumerate(self._val[val_seed]):
+                c += pooled_confusion_ref(ref.predict(v, self._embedding(ref, ("v", val_seed, i), v)), v["gt_u8"],
+                                          v["mask_values"])
+        return c
+
+    def train_steps(self, ref, seed, epoch, limit=None):
+        """One epoch (or its first `limit` steps) of oracle steps on the training seed; -> steps taken."""
+        tr = host_batches(seed, N_TRAIN, epoch)
+        k = 0
+        for i, b in enumerate(tr):
+            if limit is not None and k >= limit:
+                break
+            with oracle_mode():
+                ref.step(b, self._embedding(ref, ("t", seed, i), b))
+            k += 1
+        return k
+
+    def run(self, state, adam, train_seed, val_seed):
+        """-> ([(step, confusion [14, 4])] at CHECKPOINTS, relative decoder movement over the compared epochs)."""
+        ref = self.make(state, adam)
+        w0 = torch.cat([p.detach().flatten() for p in ref.model.mask_decoder.parameters()]).clone()
+        out = [(0, self.conf(ref, val_seed))]
+        k = 0
+        for ep in range(EPOCHS):
+            k += self.train_steps(ref, train_seed, ep)
+            out.append((k, self.conf(ref, val_seed)))
+        w1 = torch.cat([p.detach().flatten() for p in ref.model.mask_decoder.parameters()])
+        moved = float((w1 - w0).norm() / w0.norm())
+        del ref
+        torch.cuda.empty_cache()
+        return out, moved
