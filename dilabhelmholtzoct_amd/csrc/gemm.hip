@@ -108,6 +108,7 @@ struct GemmK {
   float* a_cs;   // k-major operands: per-batch column sums of A [batch][M] / B [batch][N] (or null)
   float* b_cs;
   int rgroup;    // broadcast-residual tile order (rgroup_tm); 0 = plain order
+  int res_lds;   // gemm8 in-place fp32 residual kind: residual through LDS (ph8::epilogue_res_lds)
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -1370,6 +1371,126 @@ __device__ __forceinline__ void epilogue_fast(const GemmK& p, f32x4 (&acc)[8][4]
       }
     }
 }
+// LDS-staged fp32 residual for the in-place fp32 residual kind (FE 4: the encoder's MLP2 writing the fp32 residual
+// stream, C == R): the residual of a wave's 128 x 64 tile comes in four quarters (row blocks 2q, 2q+1: 32 rows x 64
+// fp32 columns = 8 KiB) by LDS-DMA into a wave-private region, so no VGPR holds an in-flight residual and a quarter's
+// load runs under the previous quarter's arithmetic and stores (the register form waits for each half's loads with
+// the previous half's stores ahead of them in the counter). 16-B chunk c of row r sits at position c ^ (r & 15): the
+// 16 rows a ds_read_b128 lane group reads at one chunk column land on 16 distinct chunk slots.
+__device__ __forceinline__ void res_dma_q(const GemmK& p, int bz, int row0w, int col0w, int q, char* region, int lane) {
+  const int r0 = row0w + 32 * q;
+  const long long origin = (long long)bz * p.sR + (long long)r0 * p.ldr + col0w;
+  const int rows_left = max(0, p.M - r0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const float*)p.R + origin), (short)0, rows_left * (int)p.ldr * 4, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 4 * i + (lane >> 4), c = (lane & 15) ^ (r & 15);
+    // (a chunk past N reads as zero: its offset is sent past the range; its columns are never stored)
+    const uint32_t vo = col0w + 4 * c < p.N ? (uint32_t)((r * (int)p.ldr + 4 * c) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(region + i * 1024), 16, vo, 0, 0, 0);
+  }
+}
+
+template <int ACT, int Q>
+__device__ __forceinline__ void res_quarter(const GemmK& p, f32x4 (&acc)[8][4], const __amdgpu_buffer_rsrc_t& rc,
+                                            int row0w, int col0w, const float (&bv)[2][8], const char* region, int lane) {
+  const int q4 = lane >> 4;
+  const int cofs = 16 * (q4 & 1) + 8 * (q4 >> 1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int mi = 2 * Q + j;
+    const int rl = 16 * j + (lane & 15);  // row within the quarter
+    float v[2][8];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const u32x4 x = __builtin_bit_cast(u32x4, acc[mi][2 * pr]);
+      const u32x4 y = __builtin_bit_cast(u32x4, acc[mi][2 * pr + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t xi = x[i], yi = y[i];
+        const auto r = __builtin_amdgcn_permlane16_swap(xi, yi, false, false);
+        v[pr][i] = __builtin_bit_cast(float, (uint32_t)r[0]);
+        v[pr][4 + i] = __builtin_bit_cast(float, (uint32_t)r[1]);
+      }
+    }
+    // residual rows from LDS by inline asm: hipcc puts a vmcnt(0) (the next quarter's LDS-DMA in flight) in front of
+    // an ordinary LDS load; this quarter's DMA was retired by the caller's counted wait
+    f32x4 ra[2], rb[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int c0 = 8 * pr + (cofs >> 2);
+      const uint32_t base = (uint32_t)(uintptr_t)(lds_ptr_t)(region + rl * 256);
+      const uint32_t aa = base + (uint32_t)((c0 ^ (rl & 15)) << 4), ab = base + (uint32_t)(((c0 + 1) ^ (rl & 15)) << 4);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(ra[pr]) : "v"(aa));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(rb[pr]) : "v"(ab));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra[0]), "+v"(rb[0]), "+v"(ra[1]), "+v"(rb[1])::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const f32x4 a = ra[pr], b = rb[pr];
+      float o8[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o8[e] = act_apply<ACT>(v[pr][e] * p.alpha + bv[pr][e]) + a[e];
+        o8[4 + e] = act_apply<ACT>(v[pr][4 + e] * p.alpha + bv[pr][4 + e]) + b[e];
+      }
+      const uint32_t o = col0w + 32 * pr + cofs < p.N
+                             ? (uint32_t)((((Q * 32 + rl) * (int)p.ldc) + 32 * pr + cofs) * 4)
+                             : 0x80000000u;
+      const f32x4 oa = {o8[0], o8[1], o8[2], o8[3]}, ob = {o8[4], o8[5], o8[6], o8[7]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, oa), rc, o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ob), rc, o + 16, 0, 0);
+    }
+  }
+}
+
+// the four quarters: Q0 already in flight in bufX (issued during the last K-step), Q1 -> bufY, Q2 -> bufX, Q3 -> bufY,
+// each issued as soon as its region's previous quarter has been read; counted waits (each quarter's 8 stores and the
+// next quarter's 8 DMA ops may stay in flight)
+template <int ACT>
+__device__ __forceinline__ void epilogue_res_lds(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0w, int col0w,
+                                                 int lane, char* bufX, char* bufY) {
+  const int q4 = lane >> 4;
+  const int cofs = 16 * (q4 & 1) + 8 * (q4 >> 1);
+  f32x4 bt[2][2];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const int n = col0w + 32 * pr + cofs;
+    const bool ok = p.bias && n < p.N;
+    bt[pr][0] = ok ? *(const f32x4*)(p.bias + n) : (f32x4)0.0f;
+    bt[pr][1] = ok ? *(const f32x4*)(p.bias + n + 4) : (f32x4)0.0f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q0 and the bias
+  // (the bias consumed here, before any LDS-DMA is issued: hipcc waits vmcnt(0) at the first use of an ordinary load's
+  //  result while an LDS-DMA is in flight)
+  asm volatile("" : "+v"(bt[0][0]), "+v"(bt[0][1]), "+v"(bt[1][0]), "+v"(bt[1][1]));
+  float bv[2][8];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bv[pr][e] = bt[pr][0][e];
+      bv[pr][4 + e] = bt[pr][1][e];
+    }
+  const long long c_origin = (long long)bz * p.sC + (long long)row0w * p.ldc + col0w;
+  const int rows_left = max(0, p.M - row0w);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)((float*)p.C + c_origin), (short)0,
+                                                                      rows_left * (int)p.ldc * 4, 0x00020000);
+  res_dma_q(p, bz, row0w, col0w, 1, bufY, lane);
+  res_quarter<ACT, 0>(p, acc, rc, row0w, col0w, bv, bufX, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Q0 read before its region is refilled
+  res_dma_q(p, bz, row0w, col0w, 2, bufX, lane);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // Q1 (Q0's stores and Q2's DMA may stay in flight)
+  res_quarter<ACT, 1>(p, acc, rc, row0w, col0w, bv, bufY, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  res_dma_q(p, bz, row0w, col0w, 3, bufY, lane);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // Q2
+  res_quarter<ACT, 2>(p, acc, rc, row0w, col0w, bv, bufX, lane);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // Q3 (Q2's stores may stay in flight)
+  res_quarter<ACT, 3>(p, acc, rc, row0w, col0w, bv, bufY, lane);
+}
 }  // namespace ph8
 
 // TR (register epilogue): operands swapped, the accumulator holds each 16x16 block transposed
@@ -1412,6 +1533,9 @@ __device__ long long g_stamps[STAMP_WG * 4];
 template <int DBG, int EPI, int FE = 0>
 __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
   constexpr bool TR = EPI >= 0;
+  // the in-place fp32 residual kind stages its residual through LDS (ph8::epilogue_res_lds; p.res_lds, fast path
+  // bit 4096 turns it off for A/B)
+  constexpr bool RES_LDS = TR && FE == 4 && DBG == 0;
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   long long st0 = 0, st1 = 0;
@@ -1484,6 +1608,8 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
       for (int ni = 0; ni < 2; ++ni) b1[ni][kb] = ph8::frag(cb, brow + 32 + ni * 16, kb * 4 + kq);
     if (h1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // retire A-hi(t)
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (RES_LDS)  // last K-step: the first residual quarter into the buffer no K-tile needs any more
+      if (!h1 && p.res_lds) ph8::res_dma_q(p, bz, row0 + wr * 128, col0 + wc * 64, 0, nxt + wave * 8192, lane);
     raw_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     PH8_MFMA_QUAD_F(0, 1, b1, t == 0)
@@ -1520,6 +1646,13 @@ __global__ __launch_bounds__(512, 2) void gemm8_kernel(GemmK p) {
       for (int j = 0; j < 4; ++j) x += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (x == 12345.f) ((float*)p.C)[0] = x;
     return;
+  }
+  if constexpr (RES_LDS) {
+    if (p.res_lds) {  // (buffer nk & 1 holds residual quarter 0 since the last K-step; nk + 1 is free now)
+      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane, gsm + (nk & 1) * ph8::BUF + wave * 8192,
+                                 gsm + ((nk + 1) & 1) * ph8::BUF + wave * 8192);
+      return;
+    }
   }
   if constexpr (TR) {
     if constexpr (FE == 1) {
@@ -1978,6 +2111,15 @@ __global__ __launch_bounds__(256, 2) void gemm4w_kernel(GemmK p) {
     const char* cb = ca + g4::A_BYTES;
     if (t == 0) G4_STEP(ca, cb, true) else G4_STEP(ca, cb, false)
   }
+  if constexpr (FE == 4 && !CONV) {  // in-place fp32 residual (the encoder's projection): residual through LDS
+    if (p.res_lds) {
+      raw_barrier();  // every wave's reads of the ring done: 16 KiB per wave for two residual quarters
+      char* bx = gsm + wave * 16384;
+      ph8::res_dma_q(p, bz, row0 + wr * 128, col0 + wc * 64, 0, bx, lane);
+      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane, bx, bx + 8192);
+      return;
+    }
+  }
   if constexpr (FE == 1) {
     ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, lane);
   } else {
@@ -2017,6 +2159,7 @@ static int g_gemm4w = 1;
 // epilogue; fast path bit 1024 turns both off (A/B)
 static int g_gemm4w_res = 1;
 static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off: A/B)
+static int g_res_lds = 1;  // gemm8 fp32 residual kind through LDS (fast path bit 4096 turns it off: A/B)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
@@ -2399,6 +2542,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_gemm4w = (enable & 512) ? 0 : 1;
   g_gemm4w_res = (enable & 1024) ? 0 : 1;
   g_rgroup = (enable & 2048) ? 0 : 1;
+  g_res_lds = (enable & 4096) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2451,6 +2595,7 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
                  : 0;
   k.a_cs = a->a_colsum;
   k.b_cs = a->b_colsum;
+  k.res_lds = g_res_lds;
   const bool want_cs = a->a_colsum != nullptr || a->b_colsum != nullptr;
   OCTSAM_CHECK_ARG(!want_cs || (a->a_mode == 1 && a->b_mode == 1), "octsam_gemm: a_colsum / b_colsum need a_mode = b_mode = 1");
   {  // lean epilogue kind (epilogue_fast): no C_pre; a residual must have C's type, no broadcast (r_blk)

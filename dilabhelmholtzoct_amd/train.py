@@ -725,7 +725,17 @@ def training(base_model: str, config: dict, train_data=None, valid_data=None, de
     pg = process_group
     world = dist.get_world_size(pg) if pg is not None else 1
     rank = dist.get_rank(pg) if pg is not None else 0
-    device = device or torch.device("cuda", torch.cuda.current_device())
+    if device is None:
+        if not torch.cuda.is_available():
+            # the reference falls back to the CPU (training_utils.py:33); this loop's arithmetic is the HIP library
+            # (no CPU fallback by design: a silent CPU path would not be the measured product), so say so up front
+            raise RuntimeError("training() needs an MI355X (liboctsam_hip.so runs every op of the step as a HIP kernel); "
+                               "no GPU is visible. The reference's CPU step is restated as test infrastructure in "
+                               "oracle/step_ref.py (bench.py's cpu_baseline), not as a product path.")
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError(f"training() runs on a GPU device (liboctsam_hip.so), got {device}")
     model = SamModel.from_pretrained(base_model, **({"seed": config["seed"]} if "seed" in config else {})).to(device)
     if config.get("encoder_dtype", "bf16") == "fp16":  # BASELINE configs[4]
         model.set_encoder_dtype(torch.float16)

@@ -112,3 +112,18 @@ def test_save_to_disk_dataset_roundtrip(tmp_path):
         x, y = a[i], b[i]
         assert np.array_equal(x[0], y[0]) and x[1] == y[1] and x[3] == y[3]
         assert all(np.array_equal(p, q) for p, q in zip(x[2], y[2]))
+
+
+def test_training_without_gpu_raises_cleanly():
+    """train.training() has no CPU fallback (every op of the step is a HIP kernel; the reference's own CPU step is
+    oracle/step_ref.py, test infrastructure): on a host without a GPU, or asked for a CPU device, it raises with a
+    message instead of failing somewhere inside the data path (ref:octsam/models/training_utils.py:33)."""
+    import pytest
+    import torch
+    from dilabhelmholtzoct_amd.train import training
+    cfg = {"batch_size": 1, "epochs": 1, "prompt_type": "bboxes", "evaluate": False, "checkpoint": None}
+    with pytest.raises(ValueError, match="GPU device"):
+        training("facebook/sam-vit-base", cfg, [], [], device=torch.device("cpu"), log=lambda *a: None)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="needs an MI355X"):
+            training("facebook/sam-vit-base", cfg, [], [], log=lambda *a: None)

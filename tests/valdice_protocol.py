@@ -125,6 +125,10 @@ def hip_run(cuda, state, adam, train_seed, val_seed, *, epoch_batches=None, val_
     model = SamModel(NAME)
     model.load_state_dict(state)
     model = model.to(cuda)
+    if os.environ.get("OCTSAM_FUSE_DKEYS") is not None:  # A/B of a decoder rounding variant on this protocol
+        model.mask_decoder.fuse_dkeys = os.environ["OCTSAM_FUSE_DKEYS"] == "1"
+    if os.environ.get("OCTSAM_ENCODER_DTYPE") == "fp16":  # diagnostics: the fp16 encoder (BASELINE configs[4])
+        model.set_encoder_dtype(torch.float16)
     step = FusedTrainStep(model, lr=LR, topological=True, graphs=True, pipeline=True)
     step.load_optimizer_state(adam)
 
@@ -157,11 +161,16 @@ class OracleRunner:
         self.cuda = cuda
         self._emb = {}
         self._val = {}
+        self.embed_fn = None    # diagnostics (scripts/val_dice_diag.py): embeddings from elsewhere (the HIP encoder)
+        self.round_emb = False  # diagnostics: the oracle's embeddings rounded to bf16
 
     def _embedding(self, ref, key, batch):
         if key not in self._emb:
-            with oracle_mode():
-                self._emb[key] = ref.embed(batch)
+            e = self.embed_fn(batch) if self.embed_fn is not None else None
+            if e is None:
+                with oracle_mode():
+                    e = ref.embed(batch)
+            self._emb[key] = e.bfloat16().float() if self.round_emb else e
         return self._emb[key]
 
     def make(self, state, adam=None):
