@@ -103,6 +103,14 @@ _SIGNATURES = {
     "octsam_dec_t2i_bwd_sum": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                          c_void_p, c_void_p]),
+    "octsam_dec_t2i_fwd2": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "octsam_dec_t2i_bwd2": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                      c_void_p, c_void_p]),
+    "octsam_dec_t2i_bwd_sum2": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_int64, c_void_p, c_void_p]),
     "octsam_dec_i2t_fwd": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                                      c_void_p, c_int64, c_void_p]),
     "octsam_dec_i2t_bwd_partials": (c_int64, [c_int32, c_int32, c_int32]),

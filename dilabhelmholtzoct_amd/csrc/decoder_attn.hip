@@ -170,6 +170,28 @@ __device__ __forceinline__ s16x4 tr_op(const char* img, int t, int hl, bool vimg
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (lds_s16x4*)(img + 64 * r + 16 * (vimg ? vsw(r, lc) : ksw(r, lc)) + 8 * (p & 1)));
 }
+// tr_op through inline asm. hipcc puts an s_waitcnt vmcnt(0) in front of the ds_read_tr builtin whenever an LDS-DMA
+// may be in flight (it cannot tell the ring slot being loaded from the one read), which drained the K / V ring -- the
+// next steps' loads -- at every step. The slot read here is never a DMA target while it is read (each loop's
+// lgkmcnt(0) before it reissues a slot), so only the read itself is waited for: tr_wait before the values are used.
+#ifndef DEC_TR_ASM
+#define DEC_TR_ASM 1  // 0: the builtin (A/B builds)
+#endif
+__device__ __forceinline__ s16x4 tr_op_a(const char* img, int t, int hl, bool vimg, int lane) {
+  if constexpr (!DEC_TR_ASM) return tr_op(img, t, hl, vimg, lane);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r = 16 * t + 4 * g + q, lc = 2 * hl + (p >> 1);
+  const char* a = img + 64 * r + 16 * (vimg ? vsw(r, lc) : ksw(r, lc)) + 8 * (p & 1);
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(char*)a));
+  return v;
+}
+__device__ __forceinline__ void tr_wait(s16x4& a, s16x4& b) {
+  if constexpr (DEC_TR_ASM) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void tr_wait(s16x4& a, s16x4& b, s16x4& c, s16x4& d) {
+  if constexpr (DEC_TR_ASM) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
 
 // Block-diagonal token operand (x fp32 [P, Tq, 128]): lane (g, c), element j = pair dim 8g + j of column
 // n = c (n < 8: token n of head 2hp; n >= 8: token n-8 of head 2hp+1); zero off the diagonal / n >= Tq.
@@ -199,12 +221,35 @@ __device__ __forceinline__ s16x4 tokT_op(const float* x, int p, int Tq, int hp, 
   }
   return r;
 }
+// tokT_op split hi + lo (x * scale = hi + lo to ~16 mantissa bits)
+__device__ __forceinline__ void tokT_split(const float* x, int p, int Tq, int hp, int hl, float scale, int lane,
+                                           s16x4& hi, s16x4& lo) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = 4 * g + j, qi = n & 7;
+    const bool on = (n >> 3) == hl && qi < Tq;
+    const float v = on ? x[((long long)p * Tq + qi) * 128 + (2 * hp + hl) * 16 + c] * scale : 0.0f;
+    const bf16 h = (bf16)v;
+    hi[j] = __builtin_bit_cast(short, h);
+    lo[j] = __builtin_bit_cast(short, (bf16)(v - (float)h));
+  }
+}
 
 __device__ __forceinline__ s16x4 pack4(const f32x4& a) {
   s16x4 r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) r[i] = __builtin_bit_cast(short, (bf16)a[i]);
   return r;
+}
+// a = hi + lo to ~16 mantissa bits, both as bf16 MFMA operands
+__device__ __forceinline__ void split4(const f32x4& a, s16x4& hi, s16x4& lo) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16 h = (bf16)a[i];
+    hi[i] = __builtin_bit_cast(short, h);
+    lo[i] = __builtin_bit_cast(short, (bf16)(a[i] - (float)h));
+  }
 }
 __device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -226,6 +271,11 @@ __device__ __forceinline__ void wait_vm(int n) {
     T2_W(48) T2_W(52) T2_W(56) default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
   }
 #undef T2_W
+}
+// wait_vm with the loop's steady-state count tested first (one compare instead of the switch's branch tree)
+template <int FAST> __device__ __forceinline__ void wait_vm_f(int n) {
+  if (n == FAST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FAST) : "memory");
+  else wait_vm(n);
 }
 }  // namespace t2
 
@@ -257,7 +307,7 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's previous reads are done
       load_step(kb, ldkv, vb, ldkv, key0 + (s + RING - 1) * STEP, ring + ((s + RING - 1) % RING) * STEP_BYTES, lane);
     }
-    wait_vm(4 * min(RING - 1, nstep - 1 - s));
+    wait_vm_f<4 * (RING - 1)>(4 * min(RING - 1, nstep - 1 - s));
     const char* slot = ring + (s % RING) * STEP_BYTES;
     f32x4 st[2];
 #pragma unroll
@@ -291,10 +341,22 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
     l = fmaf(l, alpha, (e0[0] + e0[1]) + (e0[2] + e0[3]) + (e1[0] + e1[1]) + (e1[2] + e1[3]));
     o0 *= alpha;
     o1 *= alpha;
-    const bf16x8 pf = cat8(pack4(e0), pack4(e1));
+    // P split hi + lo as well: O feeds the backward's delta = dO . O = sum_k P_k dP_k, which must match the
+    // backward's fp32 P to the cancellation in dP - delta (a bf16 P leaves O's error at 2^-9 of the deviations of
+    // V from their P-weighted mean, which dQ = sum_k dS_k K_k then scales by |mean K| / spread of K)
+    s16x4 h0, l0, h1, l1;
+    split4(e0, h0, l0);
+    split4(e1, h1, l1);
+    const bf16x8 pf = cat8(h0, h1), pfl = cat8(l0, l1);
     const char* vimg = slot + 2048;
-    o0 = mfma32(cat8(tr_op(vimg, 0, 0, true, lane), tr_op(vimg, 1, 0, true, lane)), pf, o0);
-    o1 = mfma32(cat8(tr_op(vimg, 0, 1, true, lane), tr_op(vimg, 1, 1, true, lane)), pf, o1);
+    s16x4 a0 = tr_op_a(vimg, 0, 0, true, lane), a1 = tr_op_a(vimg, 1, 0, true, lane);
+    s16x4 a2 = tr_op_a(vimg, 0, 1, true, lane), a3 = tr_op_a(vimg, 1, 1, true, lane);
+    tr_wait(a0, a1, a2, a3);
+    const bf16x8 vt0 = cat8(a0, a1), vt1 = cat8(a2, a3);
+    o0 = mfma32(vt0, pf, o0);
+    o0 = mfma32(vt0, pfl, o0);
+    o1 = mfma32(vt1, pf, o1);
+    o1 = mfma32(vt1, pfl, o1);
   }
   l = add_xor16(l);
   l = add_xor32(l);
@@ -309,7 +371,7 @@ __global__ __launch_bounds__(256) void t2i_fwd_kernel(const float* __restrict__ 
 
 // merge the chunk partials in chunk order: out bf16 [P,Tq,128], lse fp32 [P,8,Tq] (natural log)
 __global__ void t2i_combine_kernel(const float* __restrict__ part, int nchunk, int Tq, bf16* __restrict__ out,
-                                   float* __restrict__ lse) {
+                                   float* __restrict__ lse, float* __restrict__ out_f32) {
   using namespace t2;
   const int p = blockIdx.x, t = threadIdx.x;
   const int d = t & 15, hq = t >> 4, h = hq / Tq, qi = hq - h * Tq;
@@ -325,6 +387,7 @@ __global__ void t2i_combine_kernel(const float* __restrict__ part, int nchunk, i
     O = fmaf(e, wc[n * 16 + d], O);
   }
   out[((long long)p * Tq + qi) * 128 + h * 16 + d] = (bf16)(O / Ls);
+  if (out_f32) out_f32[((long long)p * Tq + qi) * 128 + h * 16 + d] = O / Ls;  // (the backward's dO . O)
   if (d == 0) lse[((long long)p * 8 + h) * Tq + qi] = (M + __log2f(Ls)) / L2E;
 }
 
@@ -335,7 +398,7 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
                                                       int L, int nchunk, const bf16* __restrict__ out,
                                                       const float* __restrict__ dout, const float* __restrict__ lse,
                                                       bf16* __restrict__ dk, bf16* __restrict__ dv, long long lddkv,
-                                                      float* __restrict__ part) {
+                                                      float* __restrict__ part, const float* __restrict__ out_f32) {
   using namespace t2;
   extern __shared__ __attribute__((aligned(16))) char tsm[];
   const int lane = threadIdx.x & 63, hp = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
@@ -365,10 +428,16 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
     }
     l2 = lse[((long long)p * 8 + h) * Tq + qi] * L2E;
     const float* a = dout + ((long long)p * Tq + qi) * 128 + h * 16;
-    const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
     float s = 0.0f;
+    if (out_f32) {  // delta = dO . O with the forward's unrounded O (= sum_k P_k dP_k exactly, up to fp32)
+      const float* b = out_f32 + ((long long)p * Tq + qi) * 128 + h * 16;
 #pragma unroll
-    for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+      for (int d = 0; d < 16; ++d) s = fmaf(a[d], b[d], s);
+    } else {
+      const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+    }
     del = s;
   };
   float lc2, dc;
@@ -386,7 +455,7 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
     }
     // LDS-DMA loads and global stores share vmcnt; issued after step s's loads: the loads of steps
     // s+1 .. s+3 and the 8 stores of each of the steps max(0, s-3) .. s-1
-    wait_vm(4 * min(RING - 1, nstep - 1 - s) + 8 * min(RING - 1, s));
+    wait_vm_f<12 * (RING - 1)>(4 * min(RING - 1, nstep - 1 - s) + 8 * min(RING - 1, s));
     const char* slot = ring + (s % RING) * STEP_BYTES;
     const char* vimg = slot + 2048;
 #pragma unroll
@@ -394,10 +463,15 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
       const bf16x8 kf = row_op(slot, t, false, lane), vf = row_op(vimg, t, true, lane);
       f32x4 sT = mfma32(kf, qhi, (f32x4)0.0f);
       sT = mfma32(kf, qlo, sT);                     // S^T[key 4g+i][n c]
-      const f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);
+      // dP = V . dO with dO split hi + lo too: dP - delta cancels to the softmax gradient's size, so dP needs the
+      // same ~16 mantissa bits as the scores (a bf16 dO alone gave the q_proj gradient of the final token->image
+      // attention 9 % error against fp32 autograd, 50x the bf16-operand floor; scripts/grad_diag.py)
+      f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);
+      dpT = mfma32(vf, dlo, dpT);
       f32x4 sS = mfma32(qhi, kf, (f32x4)0.0f);
       sS = mfma32(qlo, kf, sS);                     // S[n 4g+i][key c]
-      const f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+      f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+      dpS = mfma32(dlo, vf, dpS);
       f32x4 dsT, pS, dsS;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -405,7 +479,9 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
         pS[i] = __builtin_amdgcn_exp2f(sS[i] - lr2[i]);
         dsS[i] = pS[i] * (dpS[i] - dr[i]);
       }
-      const s16x4 pSb = pack4(pS), dsSb = pack4(dsS), dsTb = pack4(dsT);
+      const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
+      s16x4 dsTb, dsTl;
+      split4(dsT, dsTb, dsTl);
       const long long row = ((long long)p * L + key0 + s * STEP + 16 * t + c) * lddkv + 32 * hp + 4 * g;
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl) {
@@ -414,8 +490,14 @@ __global__ __launch_bounds__(256) void t2i_bwd_kernel(const float* __restrict__ 
         *(s16x4*)(dv + row + 16 * hl) = pack4(dvt);
         *(s16x4*)(dk + row + 16 * hl) = pack4(dkt);
       }
-      dq0 = mfma16(dsTb, tr_op(slot, t, 0, false, lane), dq0);  // dQ[n 4g+i][d c] (head 2hp)
-      dq1 = mfma16(dsTb, tr_op(slot, t, 1, false, lane), dq1);  // (head 2hp+1)
+      // dQ = dS . K summed over 4096 keys whose dS sum to zero: dS split hi + lo (bf16 dS alone leaves the sum's
+      // rounding noise at the size of the result)
+      s16x4 k0 = tr_op_a(slot, t, 0, false, lane), k1 = tr_op_a(slot, t, 1, false, lane);
+      tr_wait(k0, k1);
+      dq0 = mfma16(dsTb, k0, dq0);  // dQ[n 4g+i][d c] (head 2hp)
+      dq0 = mfma16(dsTl, k0, dq0);
+      dq1 = mfma16(dsTb, k1, dq1);  // (head 2hp+1)
+      dq1 = mfma16(dsTl, k1, dq1);
     }
   }
   float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * 256;
@@ -439,15 +521,22 @@ constexpr int SMEM = 4 * WAVE_LDS;
 
 // st fp32 [P][8][Tq][2] = (lse * log2(e), dO . O) per (prompt, head, token) (the bwd kernels' row constants)
 __global__ void t2i_rowstats_kernel(const float* __restrict__ dout, const bf16* __restrict__ out,
-                                    const float* __restrict__ lse, int Tq, float* __restrict__ st) {
+                                    const float* __restrict__ lse, int Tq, float* __restrict__ st,
+                                    const float* __restrict__ out_f32) {
   const int p = blockIdx.x, t = threadIdx.x;
   if (t >= 8 * Tq) return;
   const int h = t / Tq, qi = t - h * Tq;
   const float* a = dout + ((long long)p * Tq + qi) * 128 + h * 16;
-  const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
   float s = 0.0f;
+  if (out_f32) {  // the forward's unrounded O (t2i_bwd_kernel's tok_consts)
+    const float* b = out_f32 + ((long long)p * Tq + qi) * 128 + h * 16;
 #pragma unroll
-  for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+    for (int d = 0; d < 16; ++d) s = fmaf(a[d], b[d], s);
+  } else {
+    const bf16* b = out + ((long long)p * Tq + qi) * 128 + h * 16;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) s = fmaf(a[d], (float)b[d], s);
+  }
   float* w = st + (((long long)p * 8 + h) * Tq + qi) * 2;
   w[0] = lse[((long long)p * 8 + h) * Tq + qi] * t2::L2E;
   w[1] = s;
@@ -523,7 +612,7 @@ __global__ __launch_bounds__(256) void t2i_bwd_sum_kernel(const float* __restric
   for (int pi = 0; pi < kv_rep; ++pi) {
     const int p = img * kv_rep + pi;
     if (pi + 1 < kv_rep) load_raw(p + 1, nxt);
-    bf16x8 qhi, qlo, dop;
+    bf16x8 qhi, qlo, dop, dlo;
     const float qs = 0.25f * L2E;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -531,6 +620,7 @@ __global__ __launch_bounds__(256) void t2i_bwd_sum_kernel(const float* __restric
       qhi[j] = (bf16)v8;
       qlo[j] = (bf16)(v8 - (float)qhi[j]);
       dop[j] = (bf16)cur.dv8[j];
+      dlo[j] = (bf16)(cur.dv8[j] - (float)dop[j]);
     }
     s16x4 adO[2], aQ[2];
 #pragma unroll
@@ -551,10 +641,12 @@ __global__ __launch_bounds__(256) void t2i_bwd_sum_kernel(const float* __restric
         const bf16x8 kf = row_op(slot, t, false, lane), vf = row_op(vimg, t, true, lane);
         f32x4 sT = mfma32(kf, qhi, (f32x4)0.0f);
         sT = mfma32(kf, qlo, sT);
-        const f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);
+        f32x4 dpT = mfma32(vf, dop, (f32x4)0.0f);  // (dO hi + lo: t2i_bwd_kernel)
+        dpT = mfma32(vf, dlo, dpT);
         f32x4 sS = mfma32(qhi, kf, (f32x4)0.0f);
         sS = mfma32(qlo, kf, sS);
-        const f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+        f32x4 dpS = mfma32(dop, vf, (f32x4)0.0f);
+        dpS = mfma32(dlo, vf, dpS);
         f32x4 dsT, pS, dsS;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -562,14 +654,20 @@ __global__ __launch_bounds__(256) void t2i_bwd_sum_kernel(const float* __restric
           pS[i] = __builtin_amdgcn_exp2f(sS[i] - cur.rs[i][0]);
           dsS[i] = pS[i] * (dpS[i] - cur.rs[i][1]);
         }
-        const s16x4 pSb = pack4(pS), dsSb = pack4(dsS), dsTb = pack4(dsT);
+        const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
+        s16x4 dsTb, dsTl;  // (dS hi + lo: t2i_bwd_kernel)
+        split4(dsT, dsTb, dsTl);
 #pragma unroll
         for (int hl = 0; hl < 2; ++hl) {
           adv[s2][t][hl] = mfma16(adO[hl], pSb, adv[s2][t][hl]);
           adk[s2][t][hl] = mfma16(aQ[hl], dsSb, adk[s2][t][hl]);
         }
-        dq0 = mfma16(dsTb, tr_op(slot, t, 0, false, lane), dq0);
-        dq1 = mfma16(dsTb, tr_op(slot, t, 1, false, lane), dq1);
+        s16x4 k0 = tr_op_a(slot, t, 0, false, lane), k1 = tr_op_a(slot, t, 1, false, lane);
+        tr_wait(k0, k1);
+        dq0 = mfma16(dsTb, k0, dq0);
+        dq0 = mfma16(dsTl, k0, dq0);
+        dq1 = mfma16(dsTb, k1, dq1);
+        dq1 = mfma16(dsTl, k1, dq1);
       }
     }
     float* w = part + (((long long)p * nchunk + chunk) * 4 + hp) * 256;
@@ -678,9 +776,11 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
   bf16x8 khi, klo, vop, vlo;
   tok_op(k, p, Tk, hp, 0.25f * L2E, lane, khi, klo);
   tok_op(v, p, Tk, hp, 1.0f, lane, vop, vlo);
-  s16x4 ak[2];
+  s16x4 ak[2], akl[2];
 #pragma unroll
-  for (int hl = 0; hl < 2; ++hl) ak[hl] = tokT_op(k, p, Tk, hp, hl, 0.25f, lane);  // K_h^T / 4 [d = c][n = 4g+j]
+  for (int hl = 0; hl < 2; ++hl) {
+    tokT_split(k, p, Tk, hp, hl, 0.25f, lane, ak[hl], akl[hl]);  // K_h^T / 4 [d = c][n = 4g+j]
+  }
   bool nv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) nv[i] = ((4 * g + i) & 7) < Tk;
@@ -698,7 +798,7 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
       load_step(qb, ldq, db, lddo, r0 + (s + RING - 1) * STEP, ring + ((s + RING - 1) % RING) * STEP_BYTES, lane);
     }
     // loads of steps s+1 .. s+3 and the 4 dq stores of each of the steps max(0, s-3) .. s-1 follow step s's loads
-    wait_vm(4 * min(RING - 1, nstep - 1 - s) + 4 * min(RING - 1, s));
+    wait_vm_f<8 * (RING - 1)>(4 * min(RING - 1, nstep - 1 - s) + 4 * min(RING - 1, s));
     const char* slot = ring + (s % RING) * STEP_BYTES;
     const char* dimg = slot + 2048;
 #pragma unroll
@@ -707,7 +807,10 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
       // transposed orientation [n 4g+i][r c]: softmax statistics and dQ
       f32x4 sT = mfma32(khi, qf, (f32x4)0.0f);
       sT = mfma32(klo, qf, sT);
-      const f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);
+      // dP with V hi + lo, dQ = dS K with dS and K hi + lo: dP - delta and the sum over the <= 8 tokens (whose dS sum
+      // to zero) cancel, so both carry ~16 mantissa bits (as in t2i_bwd_kernel)
+      f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);
+      dpT = mfma32(vlo, df, dpT);
       float mx = -INFINITY;
 #pragma unroll
       for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, sT[i]) : mx;
@@ -731,14 +834,20 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
       f32x4 dsT;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dsT[i] = pT[i] * (dpT[i] - del);
-      const s16x4 dsTb = pack4(dsT);
+      s16x4 dsTb, dsTl;
+      split4(dsT, dsTb, dsTl);
       bf16* dqr = dq + ((long long)p * L + r0 + s * STEP + 16 * t + c) * lddq + hp * 32 + 4 * g;
 #pragma unroll
-      for (int hl = 0; hl < 2; ++hl) *(s16x4*)(dqr + 16 * hl) = pack4(mfma16(ak[hl], dsTb, (f32x4)0.0f));
+      for (int hl = 0; hl < 2; ++hl) {
+        f32x4 a = mfma16(akl[hl], dsTb, (f32x4)0.0f);
+        a = mfma16(ak[hl], dsTl, a);
+        *(s16x4*)(dqr + 16 * hl) = pack4(mfma16(ak[hl], dsTb, a));
+      }
       // untransposed [r 4g+i][n c] for dK / dV; row statistics from lane 32 h + r (h = head of column c)
       f32x4 sS = mfma32(qf, khi, (f32x4)0.0f);
       sS = mfma32(qf, klo, sS);
-      const f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+      f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+      dpS = mfma32(df, vlo, dpS);
       f32x4 pS, dsS;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -748,11 +857,13 @@ __global__ __launch_bounds__(256) void i2t_bwd_kernel(const bf16* __restrict__ q
         dsS[i] = pS[i] * (dpS[i] - Di);
       }
       const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
-        dka[hl] = mfma16(tr_op(slot, t, hl, false, lane), dsSb, dka[hl]);  // dK^T[d 4g+i][n c] (x4)
-        dva[hl] = mfma16(tr_op(dimg, t, hl, true, lane), pSb, dva[hl]);   // dV^T[d 4g+i][n c]
-      }
+      s16x4 q0 = tr_op_a(slot, t, 0, false, lane), q1 = tr_op_a(slot, t, 1, false, lane);
+      s16x4 o0 = tr_op_a(dimg, t, 0, true, lane), o1 = tr_op_a(dimg, t, 1, true, lane);
+      tr_wait(q0, q1, o0, o1);
+      dka[0] = mfma16(q0, dsSb, dka[0]);  // dK^T[d 4g+i][n c] (x4)
+      dva[0] = mfma16(o0, pSb, dva[0]);   // dV^T[d 4g+i][n c]
+      dka[1] = mfma16(q1, dsSb, dka[1]);
+      dva[1] = mfma16(o1, pSb, dva[1]);
     }
   }
   if (cv) {
@@ -852,7 +963,7 @@ __global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict
       load_rows32(dbase(p + 1), lddo, r0 + STEP, nb + 2048, true, lane);
       load_raw(p + 1, nxt);
     }
-    bf16x8 khi, klo, vop;
+    bf16x8 khi, klo, vop, vlo;
     const float ks = 0.25f * L2E;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -860,12 +971,18 @@ __global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict
       khi[j] = (bf16)x;
       klo[j] = (bf16)(x - (float)khi[j]);
       vop[j] = (bf16)cur.vv[j];
+      vlo[j] = (bf16)(cur.vv[j] - (float)vop[j]);
     }
-    s16x4 ak[2];
+    s16x4 ak[2], akl[2];
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ak[hl][j] = __builtin_bit_cast(short, (bf16)(cur.kT[hl][j] * 0.25f));
+      for (int j = 0; j < 4; ++j) {
+        const float x = cur.kT[hl][j] * 0.25f;
+        const bf16 hi = (bf16)x;
+        ak[hl][j] = __builtin_bit_cast(short, hi);
+        akl[hl][j] = __builtin_bit_cast(short, (bf16)(x - (float)hi));
+      }
     f32x4 dka[2], dva[2];
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl) dka[hl] = dva[hl] = (f32x4)0.0f;
@@ -879,7 +996,8 @@ __global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict
         const bf16x8 qf = row_op(slot, t, false, lane), df = row_op(dimg, t, true, lane);
         f32x4 sT = mfma32(khi, qf, (f32x4)0.0f);
         sT = mfma32(klo, qf, sT);
-        const f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);
+        f32x4 dpT = mfma32(vop, df, (f32x4)0.0f);  // (V, dS and K hi + lo: i2t_bwd_kernel)
+        dpT = mfma32(vlo, df, dpT);
         float mx = -INFINITY;
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = nv[i] ? fmaxf(mx, sT[i]) : mx;
@@ -903,12 +1021,18 @@ __global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict
         f32x4 dsT;
 #pragma unroll
         for (int i = 0; i < 4; ++i) dsT[i] = pT[i] * (dpT[i] - del);
-        const s16x4 dsTb = pack4(dsT);
+        s16x4 dsTb, dsTl;
+        split4(dsT, dsTb, dsTl);
 #pragma unroll
-        for (int hl = 0; hl < 2; ++hl) adq[s2][t][hl] = mfma16(ak[hl], dsTb, adq[s2][t][hl]);
+        for (int hl = 0; hl < 2; ++hl) {
+          adq[s2][t][hl] = mfma16(akl[hl], dsTb, adq[s2][t][hl]);
+          adq[s2][t][hl] = mfma16(ak[hl], dsTl, adq[s2][t][hl]);
+          adq[s2][t][hl] = mfma16(ak[hl], dsTb, adq[s2][t][hl]);
+        }
         f32x4 sS = mfma32(qf, khi, (f32x4)0.0f);
         sS = mfma32(qf, klo, sS);
-        const f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+        f32x4 dpS = mfma32(df, vop, (f32x4)0.0f);
+        dpS = mfma32(df, vlo, dpS);
         f32x4 pS, dsS;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -918,11 +1042,13 @@ __global__ __launch_bounds__(256) void i2t_bwd_sum_kernel(const bf16* __restrict
           dsS[i] = pS[i] * (dpS[i] - Di);
         }
         const s16x4 pSb = pack4(pS), dsSb = pack4(dsS);
-#pragma unroll
-        for (int hl = 0; hl < 2; ++hl) {
-          dka[hl] = mfma16(tr_op(slot, t, hl, false, lane), dsSb, dka[hl]);
-          dva[hl] = mfma16(tr_op(dimg, t, hl, true, lane), pSb, dva[hl]);
-        }
+        s16x4 q0 = tr_op_a(slot, t, 0, false, lane), q1 = tr_op_a(slot, t, 1, false, lane);
+        s16x4 o0 = tr_op_a(dimg, t, 0, true, lane), o1 = tr_op_a(dimg, t, 1, true, lane);
+        tr_wait(q0, q1, o0, o1);
+        dka[0] = mfma16(q0, dsSb, dka[0]);
+        dva[0] = mfma16(o0, pSb, dva[0]);
+        dka[1] = mfma16(q1, dsSb, dka[1]);
+        dva[1] = mfma16(o1, pSb, dva[1]);
       }
     }
     if (cv) {
@@ -979,9 +1105,10 @@ static void t2i_smem_attr() {
   }
 }
 
-extern "C" int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
-                                       int32_t P, int32_t Tq, int32_t L, const float* score_bias, void* out, float* lse,
-                                       float* workspace, void* stream) {
+// out_f32 (optional, fp32 [P, Tq, 128]): the unrounded O as well, for the backward's delta = dO . O
+extern "C" int octsam_dec_t2i_fwd2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                                   int32_t Tq, int32_t L, const float* score_bias, void* out, float* out_f32, float* lse,
+                                   float* workspace, void* stream) {
   OCTSAM_CHECK_ARG(q && k && v && out && lse && workspace && P > 0 && Tq > 0 && Tq <= MAXT && L > 0 && L % 32 == 0 &&
                        kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 && (uintptr_t)k % 16 == 0 &&
                        (uintptr_t)v % 16 == 0 && (uintptr_t)score_bias % 16 == 0,
@@ -992,9 +1119,16 @@ extern "C" int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void
   hipLaunchKernelGGL(t2i_fwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, s, q, (const bf16*)k, (const bf16*)v, ldkv,
                      kv_rep, Tq, L, nch, workspace, score_bias);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
-  hipLaunchKernelGGL(t2i_combine_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)out, lse);
+  hipLaunchKernelGGL(t2i_combine_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)out, lse,
+                     out_f32);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_fwd");
   return 0;
+}
+
+extern "C" int octsam_dec_t2i_fwd_bias(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
+                                       int32_t P, int32_t Tq, int32_t L, const float* score_bias, void* out, float* lse,
+                                       float* workspace, void* stream) {
+  return octsam_dec_t2i_fwd2(q, k, v, ldkv, kv_rep, P, Tq, L, score_bias, out, nullptr, lse, workspace, stream);
 }
 
 extern "C" int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
@@ -1002,9 +1136,11 @@ extern "C" int octsam_dec_t2i_fwd(const float* q, const void* k, const void* v, 
   return octsam_dec_t2i_fwd_bias(q, k, v, ldkv, kv_rep, P, Tq, L, nullptr, out, lse, workspace, stream);
 }
 
-extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
-                                  int32_t Tq, int32_t L, const void* out, const float* dout, const float* lse, void* dq,
-                                  void* dk, void* dv, int64_t lddkv, float* workspace, void* stream) {
+// out_f32: the forward's fp32 O (octsam_dec_t2i_fwd2) for delta, or null (delta from the bf16 out)
+extern "C" int octsam_dec_t2i_bwd2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                                   int32_t Tq, int32_t L, const void* out, const float* out_f32, const float* dout,
+                                   const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace,
+                                   void* stream) {
   OCTSAM_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv && workspace && P > 0 && Tq > 0 &&
                        Tq <= MAXT && L > 0 && L % 32 == 0 && kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 &&
                        lddkv % 4 == 0 && (uintptr_t)k % 16 == 0 && (uintptr_t)v % 16 == 0 &&
@@ -1014,11 +1150,18 @@ extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, 
   const int nch = t2i_nchunk(L);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(t2i_bwd_kernel, dim3(P * nch), dim3(256), t2::SMEM, s, q, (const bf16*)k, (const bf16*)v, ldkv,
-                     kv_rep, Tq, L, nch, (const bf16*)out, dout, lse, (bf16*)dk, (bf16*)dv, lddkv, workspace);
+                     kv_rep, Tq, L, nch, (const bf16*)out, dout, lse, (bf16*)dk, (bf16*)dv, lddkv, workspace, out_f32);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
   hipLaunchKernelGGL(t2i_dq_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, workspace, nch, Tq, (bf16*)dq);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd");
   return 0;
+}
+
+extern "C" int octsam_dec_t2i_bwd(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                                  int32_t Tq, int32_t L, const void* out, const float* dout, const float* lse, void* dq,
+                                  void* dk, void* dv, int64_t lddkv, float* workspace, void* stream) {
+  return octsam_dec_t2i_bwd2(q, k, v, ldkv, kv_rep, P, Tq, L, out, nullptr, dout, lse, dq, dk, dv, lddkv, workspace,
+                             stream);
 }
 
 // the shared-K/V backward with the prompt sum fused in (t2i_bwd_sum_kernel): dk / dv are the IMAGE rows
@@ -1027,10 +1170,10 @@ extern "C" int64_t octsam_dec_t2i_bwd_sum_workspace(int32_t P, int32_t Tq, int32
   return (int64_t)P * (L / t2s::SCH) * 4 * 256 + (int64_t)P * 8 * Tq * 2;
 }
 
-extern "C" int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
-                                      int32_t P, int32_t Tq, int32_t L, const void* out, const float* dout,
-                                      const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace,
-                                      void* stream) {
+extern "C" int octsam_dec_t2i_bwd_sum2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
+                                       int32_t P, int32_t Tq, int32_t L, const void* out, const float* out_f32,
+                                       const float* dout, const float* lse, void* dq, void* dk, void* dv, int64_t lddkv,
+                                       float* workspace, void* stream) {
   OCTSAM_CHECK_ARG(q && k && v && out && dout && lse && dq && dk && dv && workspace && P > 0 && Tq > 0 &&
                        Tq <= MAXT && L > 0 && L % t2s::SCH == 0 && kv_rep > 0 && P % kv_rep == 0 && ldkv % 8 == 0 &&
                        lddkv % 4 == 0 && (uintptr_t)k % 16 == 0 && (uintptr_t)v % 16 == 0 &&
@@ -1045,7 +1188,7 @@ extern "C" int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void*
   float* part = workspace;
   float* st = workspace + (int64_t)P * nch * 4 * 256;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(t2i_rowstats_kernel, dim3(P), dim3(64), 0, s, dout, (const bf16*)out, lse, Tq, st);
+  hipLaunchKernelGGL(t2i_rowstats_kernel, dim3(P), dim3(64), 0, s, dout, (const bf16*)out, lse, Tq, st, out_f32);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd_sum");
   hipLaunchKernelGGL(t2i_bwd_sum_kernel, dim3(nimg * nch), dim3(256), t2s::SMEM, s, q, (const bf16*)k, (const bf16*)v,
                      ldkv, kv_rep, Tq, L, nch, dout, st, (bf16*)dk, (bf16*)dv, lddkv, part);
@@ -1053,6 +1196,14 @@ extern "C" int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void*
   hipLaunchKernelGGL(t2i_dq_kernel, dim3(P), dim3(8 * Tq * 16), 0, s, part, nch, Tq, (bf16*)dq);
   OCTSAM_LAUNCH_CHECK("octsam_dec_t2i_bwd_sum");
   return 0;
+}
+
+extern "C" int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep,
+                                      int32_t P, int32_t Tq, int32_t L, const void* out, const float* dout,
+                                      const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace,
+                                      void* stream) {
+  return octsam_dec_t2i_bwd_sum2(q, k, v, ldkv, kv_rep, P, Tq, L, out, nullptr, dout, lse, dq, dk, dv, lddkv, workspace,
+                                 stream);
 }
 
 static int i2t_nchunk(int L) { return (L + i2::CHUNK - 1) / i2::CHUNK; }

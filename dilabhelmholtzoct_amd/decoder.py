@@ -535,8 +535,9 @@ class MaskDecoder(nn.Module):
             ls.KQV, ls.kv_src_b, ls.kv_rep = KQV, src_b, kv_rep
             to_b = torch.empty(R, CI, device=dev, dtype=b16)
             lse = torch.empty(P, 8, T, device=dev, dtype=f32)
-            K.t2i_fwd(Q, KQV, KQV[:, 2 * CI:], 3 * CI, kv_rep, P, T, L, to_b, lse, score_bias=sbias)
-            ls.t2i_Q, ls.t2i_o_b, ls.t2i_lse = Q, to_b, lse
+            to_f = torch.empty(R, CI, device=dev, dtype=f32)  # unrounded O: the backward's delta = dO . O
+            K.t2i_fwd(Q, KQV, KQV[:, 2 * CI:], 3 * CI, kv_rep, P, T, L, to_b, lse, score_bias=sbias, out_f32=to_f)
+            ls.t2i_Q, ls.t2i_o_b, ls.t2i_o_f, ls.t2i_lse = Q, to_b, to_f, lse
             s2 = self._lin(to_b, t2i + "out_proj.weight", t2i + "out_proj.bias",
                            torch.empty(R, C, device=dev, dtype=f32), R, residual=queries)
             queries, queries_b, ls.ln2 = self._ln(s2, pre + "layer_norm2", eps, R)
@@ -577,7 +578,8 @@ class MaskDecoder(nn.Module):
         s.f_KV = KV
         s.f_o_b = torch.empty(R, CI, device=dev, dtype=b16)
         s.f_lse = torch.empty(P, 8, T, device=dev, dtype=f32)
-        K.t2i_fwd(s.f_Q, KV, KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, s.f_lse)
+        s.f_o_f = torch.empty(R, CI, device=dev, dtype=f32)
+        K.t2i_fwd(s.f_Q, KV, KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, s.f_lse, out_f32=s.f_o_f)
         sf = self._lin(s.f_o_b, f + "out_proj.weight", f + "out_proj.bias", torch.empty(R, C, device=dev, dtype=f32), R,
                        residual=queries)
         q7, q7_b, s.lnf = self._ln(sf, tr + "layer_norm_final_attn", 1e-5, R)
@@ -694,7 +696,8 @@ class MaskDecoder(nn.Module):
             dKV, lkv = dup1pre[:, 256:], 512
         else:
             dKV, lkv = torch.empty(RL, 2 * CI, device=dev, dtype=b16), 2 * CI
-        K.t2i_bwd(s.f_Q, s.f_KV, s.f_KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, dfo, s.f_lse, dQ, dKV, dKV[:, CI:], lkv)
+        K.t2i_bwd(s.f_Q, s.f_KV, s.f_KV[:, CI:], 2 * CI, 1, P, T, L, s.f_o_b, dfo, s.f_lse, dQ, dKV, dKV[:, CI:], lkv,
+                  out_f32=s.f_o_f)
         self._qin_bwd(dQ, s.f_qin_b, f + "q_proj.weight", f + "q_proj.bias", R, dq, dtok)
         # d keys2 += [dK | dV] @ [Wk; Wv]
         wkv = self._group(self.flat_b16, [f + "k_proj.weight", f + "v_proj.weight"], C)
@@ -759,14 +762,14 @@ class MaskDecoder(nn.Module):
                 # K / V shared by the image's prompts: their gradients summed over the prompts inside the kernel
                 dKV_img = torch.empty(B * L, 2 * CI, device=dev, dtype=b16)
                 K.t2i_bwd_sum(ls.t2i_Q, KQV, KQV[:, 2 * CI:], 3 * CI, ls.kv_rep, P, T, L, ls.t2i_o_b, dto, ls.t2i_lse,
-                              dQ, dKV_img, dKV_img[:, CI:], 2 * CI)
+                              dQ, dKV_img, dKV_img[:, CI:], 2 * CI, out_f32=ls.t2i_o_f)
             elif li == 0:
                 dKV0 = torch.empty(RL, 2 * CI, device=dev, dtype=b16)
                 K.t2i_bwd(ls.t2i_Q, KQV, KQV[:, 2 * CI:], 3 * CI, ls.kv_rep, P, T, L, ls.t2i_o_b, dto, ls.t2i_lse, dQ,
-                          dKV0, dKV0[:, CI:], 2 * CI)
+                          dKV0, dKV0[:, CI:], 2 * CI, out_f32=ls.t2i_o_f)
             else:
                 K.t2i_bwd(ls.t2i_Q, KQV, KQV[:, 2 * CI:], 3 * CI, 1, P, T, L, ls.t2i_o_b, dto, ls.t2i_lse, dQ, dKQV,
-                          dKQV[:, 2 * CI:], 3 * CI)
+                          dKQV[:, 2 * CI:], 3 * CI, out_f32=ls.t2i_o_f)
             self._qin_bwd(dQ, ls.t2i_qin_b, t2i + "q_proj.weight", t2i + "q_proj.bias", R, dq, dtok)
             # image-side projections of this block's input keys
             kq = [t2i + "k_proj.weight", i2t + "q_proj.weight"]

@@ -306,34 +306,51 @@ def _t2i_workspace(P, L, device):
     return torch.empty(n, device=device, dtype=torch.float32)
 
 
-def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse, score_bias=None):
-    """score_bias: fp32 [P, L] added to the logits (attention_similarity), or None."""
+def _opt(t):
+    return ptr(t) if t is not None else None
+
+
+def t2i_fwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, lse, score_bias=None, out_f32=None):
+    """score_bias: fp32 [P, L] added to the logits (attention_similarity), or None. out_f32: fp32 [P, Tq, 128] that
+    also receives the unrounded O (for the backward's delta), or None (octsam_dec_t2i_fwd2)."""
     _require_cuda(q, k, v, out, lse)
     ws = _t2i_workspace(P, L, q.device)
-    if score_bias is None:
-        _lib.call("octsam_dec_t2i_fwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(lse), ptr(ws))
-    else:
-        if score_bias.dtype != torch.float32 or score_bias.numel() != P * L or not score_bias.is_contiguous():
-            raise ValueError("t2i_fwd: score_bias must be contiguous fp32 [P, L]")
-        _lib.call("octsam_dec_t2i_fwd_bias", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(score_bias),
-                  ptr(out), ptr(lse), ptr(ws))
+    if score_bias is not None and (score_bias.dtype != torch.float32 or score_bias.numel() != P * L
+                                   or not score_bias.is_contiguous()):
+        raise ValueError("t2i_fwd: score_bias must be contiguous fp32 [P, L]")
+    if out_f32 is not None:
+        _require_cuda(out_f32)
+        if out_f32.dtype != torch.float32 or out_f32.numel() != P * Tq * 128 or not out_f32.is_contiguous():
+            raise ValueError("t2i_fwd: out_f32 must be contiguous fp32 [P, Tq, 128]")
+    _lib.call("octsam_dec_t2i_fwd2", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, _opt(score_bias), ptr(out),
+              _opt(out_f32), ptr(lse), ptr(ws))
 
 
-def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
+def _check_out_f32(out_f32, P, Tq):
+    if out_f32 is not None:
+        _require_cuda(out_f32)
+        if out_f32.dtype != torch.float32 or out_f32.numel() != P * Tq * 128 or not out_f32.is_contiguous():
+            raise ValueError("t2i backward: out_f32 must be contiguous fp32 [P, Tq, 128]")
+
+
+def t2i_bwd(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv, out_f32=None):
+    """out_f32: the forward's fp32 O (t2i_fwd(out_f32=...)) for delta = dO . O, or None (from the bf16 out)."""
     _require_cuda(q, k, v, out, dout, lse, dq, dk, dv)
+    _check_out_f32(out_f32, P, Tq)
     ws = _t2i_workspace(P, L, q.device)
-    _lib.call("octsam_dec_t2i_bwd", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(dout), ptr(lse),
-              ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
+    _lib.call("octsam_dec_t2i_bwd2", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), _opt(out_f32),
+              ptr(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
 
 
-def t2i_bwd_sum(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv):
+def t2i_bwd_sum(q, k, v, ldkv, kv_rep, P, Tq, L, out, dout, lse, dq, dk, dv, lddkv, out_f32=None):
     """t2i_bwd for K / V shared by kv_rep prompts per image with the prompt sum fused in: dk, dv are the image rows
-    [(P / kv_rep) * L, lddkv] (octsam_dec_t2i_bwd_sum)."""
+    [(P / kv_rep) * L, lddkv] (octsam_dec_t2i_bwd_sum2)."""
     _require_cuda(q, k, v, out, dout, lse, dq, dk, dv)
+    _check_out_f32(out_f32, P, Tq)
     n = _lib.load().octsam_dec_t2i_bwd_sum_workspace(P, Tq, L)
     ws = torch.empty(n, device=q.device, dtype=torch.float32)
-    _lib.call("octsam_dec_t2i_bwd_sum", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), ptr(dout), ptr(lse),
-              ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
+    _lib.call("octsam_dec_t2i_bwd_sum2", ptr(q), ptr(k), ptr(v), ldkv, kv_rep, P, Tq, L, ptr(out), _opt(out_f32),
+              ptr(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv), lddkv, ptr(ws))
 
 
 def i2t_fwd(q, ldq, q_rep, k, v, P, Tk, L, out, ldo):

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 20
+#define OCTSAM_ABI_VERSION 21
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -286,6 +286,20 @@ int64_t octsam_dec_t2i_bwd_sum_workspace(int32_t P, int32_t Tq, int32_t L);
 int octsam_dec_t2i_bwd_sum(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
                            int32_t Tq, int32_t L, const void* out, const float* dout, const float* lse, void* dq,
                            void* dk, void* dv, int64_t lddkv, float* workspace, void* stream);
+/* The same three with the forward's unrounded O (ABI 21): octsam_dec_t2i_fwd2 also writes out_f32 fp32 [P,Tq,128]
+ * (or null: = octsam_dec_t2i_fwd_bias); the backward variants take it for the row constant delta = dO . O (null: from
+ * the bf16 out). The training step uses these: the backward's dP - delta cancels to the size of the softmax gradient,
+ * and a bf16 O leaves delta's rounding at that size. All t2i backward variants split dO and dS into bf16 hi + lo. */
+int octsam_dec_t2i_fwd2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                        int32_t Tq, int32_t L, const float* score_bias, void* out, float* out_f32, float* lse,
+                        float* workspace, void* stream);
+int octsam_dec_t2i_bwd2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                        int32_t Tq, int32_t L, const void* out, const float* out_f32, const float* dout,
+                        const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace, void* stream);
+int octsam_dec_t2i_bwd_sum2(const float* q, const void* k, const void* v, int64_t ldkv, int32_t kv_rep, int32_t P,
+                            int32_t Tq, int32_t L, const void* out, const float* out_f32, const float* dout,
+                            const float* lse, void* dq, void* dk, void* dv, int64_t lddkv, float* workspace,
+                            void* stream);
 int octsam_dec_i2t_fwd(const void* q, int64_t ldq, int32_t q_rep, const float* k, const float* v, int32_t P, int32_t Tk,
                        int32_t L, void* out, int64_t ldo, void* stream);
 int64_t octsam_dec_i2t_bwd_partials(int32_t P, int32_t Tk, int32_t L);

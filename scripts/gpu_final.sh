@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-4 snapshot on the GPU box (outputs under gpurun_out/$TAG; smoke + pytest -m gpu run separately by
-# scripts/gpu_r04_tests.sh): the two PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs on gfx950) over a short eager
+# Round-end snapshot on the GPU box (outputs under gpurun_out/$TAG; smoke + pytest -m gpu run separately by
+# scripts/gpu_tests_final.sh): the two PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs on gfx950) over a short eager
 # bench -> the GEMM family's HBM bytes per launch (traffic_gemm_family.json: gemm8 + gemm8p + gemm4w, the launch set of
 # roofline.compulsory_bytes_per_launch; copied into profiles/ on the box so the bench below reads it) and the
 # per-kernel traffic table; then the bench (default flags) and rocprofv3 kernel-trace/stats of the bench (pipelined)
 # and of the sequential step.
 set -u
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${TAG:-r04final}
+O=$R/gpurun_out/${TAG:-final}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 SHORT="--eager --steps 2 --warmup 1 --cpu-baseline 0 --val 0 --val-protocol 0 --top-off 0 --roof-steps 0 --data-path 0 --e2e-steps 0 --topo-all 0 --loop-images 0"
