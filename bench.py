@@ -428,33 +428,15 @@ def val_protocol(args, device):
     state), then per (training, held-out) seed pair 4 epochs (64 steps) on 128 scans, the 32 held-out scans scored
     after every epoch, beside the fp32 oracle's values from the same start (tests/golden/valdice_oracle.json, made by
     tests/golden/make_valdice_golden.py on MI355X with the oracle alone, so they hold for any HIP build). Batches come
-    from the HIP data path (bit-identical to the host SAMDataset + collate + SamProcessor path the test uses:
-    test_gpu_training_loop.py); the step is the benchmarked one (hipGraphs + encoder lookahead)."""
+    from the HIP data path as in the test (valdice_protocol.device_batches: bit-identical to the host SAMDataset +
+    collate + SamProcessor path, test_gpu_training_loop.py); the step is the benchmarked one (hipGraphs + encoder
+    lookahead)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import valdice_protocol as P
-    from dilabhelmholtzoct_amd import data
-    from dilabhelmholtzoct_amd.components import collate_device
-    from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
     gold = json.load(open(P.ORACLE_JSON))
     gold_pairs = {(g["train_seed"], g["val_seed"]): g for g in gold["pairs"]}
     t0 = time.perf_counter()
-    dproc = DeviceProcessor(device)
-    raw = {}
-
-    def epoch_batches(seed, n, epoch):
-        if seed not in raw:
-            ds = data.synthetic_oct(seed=seed, n=n)
-            raw[seed] = (np.stack([np.array(d["image"]) for d in ds]), np.stack([np.array(d["label"]) for d in ds]))
-        imgs, labs = raw[seed]
-        out = []
-        for s in range(0, n, P.BS):
-            e = min(n, s + P.BS)
-            hooks = [(lambda i=i: data.seed_sample(epoch, i, seed)) for i in range(s, e)]
-            b = collate_device(imgs[s:e], labs[s:e], "bboxes", device, seed_hooks=hooks, processor=dproc)
-            b.pop("prompt_raw", None)
-            out.append(b)
-        return out
-
+    epoch_batches = P.device_batches(device)
     state, adam = P.load_warm()
     pairs = []
     for tr, va in P.SEEDS:

@@ -58,24 +58,32 @@ def make_warm(cuda, out):
                       "val_dice_seed3000": round(d, 5)}), flush=True)
 
 
-def make_oracle(cuda, out):
+def make_oracle(cuda, out, keep=False, n_perturb=N_PERTURB):
+    """keep: pairs already in `out` are kept as they are (only the missing ones are run); n_perturb: perturbed runs
+    per new pair (0: no spread for it)."""
     from oracle.eval_ref import mean_specificity_ref
     state, adam = P.load_warm()
     runner = P.OracleRunner(cuda)
+    old = {}
+    if keep and os.path.exists(out):
+        old = {(g["train_seed"], g["val_seed"]): g for g in json.load(open(out))["pairs"]}
     pairs = []
     t0 = time.time()
     for tr, va in P.SEEDS:
+        if (tr, va) in old:
+            pairs.append(old[tr, va])
+            continue
         base, moved = runner.run(state, adam, tr, va)
         rec = {"train_seed": tr, "val_seed": va, "steps": [k for k, _ in base],
                "oracle_dice": [round(P.dice_of(c), 5) for _, c in base],
                "oracle_specificity": round(mean_specificity_ref(base[-1][1]), 4), "oracle_moved": round(moved, 4)}
         spread = []
-        for j in range(N_PERTURB):
+        for j in range(n_perturb):
             pert, _ = runner.run(P.perturbed(state, 100 + j), adam, tr, va)
             spread.append([round(P.dice_of(c), 5) for _, c in pert])
         rec["perturbed_dice"] = spread
-        rec["spread"] = [round(max([b] + [s[i] for s in spread]) - min([b] + [s[i] for s in spread]), 5)
-                         for i, b in enumerate(rec["oracle_dice"])]
+        rec["spread"] = ([round(max([b] + [s[i] for s in spread]) - min([b] + [s[i] for s in spread]), 5)
+                          for i, b in enumerate(rec["oracle_dice"])] if spread else None)
         pairs.append(rec)
         print(json.dumps(rec), flush=True)
     n = len(pairs)
@@ -90,7 +98,8 @@ def make_oracle(cuda, out):
                       "MIOpen off, torch deterministic algorithms); depends on no HIP kernel",
            "steps": P.CHECKPOINTS, "pairs": pairs, "oracle_mean_dice": mean,
            "noise_floor": f"per pair, spread = max - min of the oracle's Dice over the base run and {N_PERTURB} runs "
-                          "from the start state with every decoder weight times (1 + 2^-8 u), u ~ U(-1, 1)",
+                          "from the start state with every decoder weight times (1 + 2^-8 u), u ~ U(-1, 1) (the first six "
+                          "pairs; null for pairs made without perturbed runs)",
            "seconds": round(time.time() - t0, 1)}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
@@ -103,12 +112,14 @@ def main():
     p.add_argument("--oracle", action="store_true")
     p.add_argument("--warm-out", default=P.WARM)
     p.add_argument("--oracle-out", default=P.ORACLE_JSON)
+    p.add_argument("--keep", action="store_true", help="--oracle: keep the pairs already in --oracle-out")
+    p.add_argument("--perturb", type=int, default=N_PERTURB, help="--oracle: perturbed runs per new pair")
     a = p.parse_args()
     cuda = torch.device("cuda", 0)
     if a.warm:
         make_warm(cuda, a.warm_out)
     if a.oracle:
-        make_oracle(cuda, a.oracle_out)
+        make_oracle(cuda, a.oracle_out, keep=a.keep, n_perturb=a.perturb)
 
 
 if __name__ == "__main__":
