@@ -53,6 +53,8 @@ _SIGNATURES = {
     "octsam_wgrad_supported": (c_int32, [c_int64, c_int32, c_int32]),
     "octsam_wgrad_tok": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_float,
                                    c_void_p, c_void_p]),
+    "octsam_wgrad_tok_group": (c_int32, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "octsam_wgrad_workspace": (c_int64, [c_int64, c_int32, c_int32]),
     "octsam_wgrad": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p, c_float,
                                c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),

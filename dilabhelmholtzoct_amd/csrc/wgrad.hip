@@ -228,15 +228,14 @@ __device__ __forceinline__ void tok_load(__amdgpu_buffer_rsrc_t rs, int voff, in
 }
 }  // namespace tok
 
+// one 32 x 32 output tile (tile = to * tiles_i + ti) of one token-side problem
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restrict__ dy, long long ldy,
-                                                            const bf16* __restrict__ x, long long ldx, long long M,
-                                                            int tiles_i, float* __restrict__ out, int ldo, float beta,
-                                                            float* __restrict__ db) {
+__device__ __forceinline__ void tok_tile(const bf16* __restrict__ dy, long long ldy, const bf16* __restrict__ x,
+                                         long long ldx, long long M, int tile, int tiles_i, float* __restrict__ out,
+                                         int ldo, float beta, float* __restrict__ db, char* smem) {
   using namespace tok;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int to = blockIdx.x / tiles_i, ti = blockIdx.x - to * tiles_i;
+  const int to = tile / tiles_i, ti = tile - to * tiles_i;
   const int o0 = to * 32, i0 = ti * 32;
   // this wave's rows: [m_beg, m_end), 32-row multiples except the last range
   const long long per = ((M + NW - 1) / NW + SROWS - 1) / SROWS * SROWS;
@@ -309,6 +308,44 @@ __global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restri
   }
 }
 
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restrict__ dy, long long ldy,
+                                                            const bf16* __restrict__ x, long long ldx, long long M,
+                                                            int tiles_i, float* __restrict__ out, int ldo, float beta,
+                                                            float* __restrict__ db) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tok_tile<NW>(dy, ldy, x, ldx, M, blockIdx.x, tiles_i, out, ldo, beta, db, smem);
+}
+
+// Several independent token-side problems in one launch (the decoder backward's weight gradients, deferred and
+// issued together: one launch instead of one ~18 us latency-bound launch per weight): workgroup b takes tile
+// b - start[k] of problem k, start[k] <= b < start[k + 1]. Problems of one group never share an output (the host
+// flushes a group before a problem that overlaps a pending one's out / db).
+constexpr int TOK_GROUP_MAX = 24;
+struct TokProb {
+  const bf16* dy;
+  const bf16* x;
+  float* out;
+  float* db;
+  long long ldy, ldx, M;
+  int tiles_i, ldo;
+  float beta;
+};
+struct TokGroup {
+  TokProb p[TOK_GROUP_MAX];
+  int start[TOK_GROUP_MAX + 1];
+  int n;
+};
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_tok_group_kernel(const TokGroup g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < g.n && g.start[k + 1] <= b) ++k;
+  const TokProb& q = g.p[k];
+  tok_tile<NW>(q.dy, q.ldy, q.x, q.ldx, q.M, b - g.start[k], q.tiles_i, q.out, q.ldo, q.beta, q.db, smem);
+}
+
 int n_workgroups(long long M, long long& rows_per) {
   static int n_cu = 0;
   if (!n_cu) {
@@ -367,6 +404,50 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
                        (const bf16*)x, (long long)ldx, (long long)M, I / 32, out, I, beta, db);
   }
   OCTSAM_LAUNCH_CHECK("octsam_wgrad_tok");
+  return 0;
+}
+
+template <int NW>
+void launch_tok_group(TokGroup& g, hipStream_t s) {
+  for (int k = g.n + 1; k <= TOK_GROUP_MAX; ++k) g.start[k] = g.start[g.n];
+  constexpr int LDS = NW * tok::NST * tok::STB;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_tok_group_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad_tok_group_kernel<NW>, dim3(g.start[g.n]), dim3(NW * 64), LDS, s, g);
+}
+
+extern "C" int octsam_wgrad_tok_group(int32_t n, const void* const* dy, const int64_t* ldy, const void* const* x,
+                                      const int64_t* ldx, const int64_t* M, const int32_t* O, const int32_t* I,
+                                      float* const* out, const float* beta, float* const* db, void* stream) {
+  OCTSAM_CHECK_ARG(n > 0 && n <= TOK_GROUP_MAX && dy && ldy && x && ldx && M && O && I && out && beta && db,
+                   "octsam_wgrad_tok_group: n=%d (1..%d) and every array non-null", n, TOK_GROUP_MAX);
+  // two launches at most: the problems octsam_wgrad_tok runs with 8 waves (M > 1024) and with 4, so that every
+  // problem keeps its single-launch partition of the rows (same bits)
+  TokGroup g8, g4;
+  g8.n = g4.n = 0;
+  g8.start[0] = g4.start[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    OCTSAM_CHECK_ARG(dy[k] && x[k] && out[k] && M[k] > 0 && M[k] < (1LL << 24) && O[k] > 0 && I[k] > 0 &&
+                         O[k] % 32 == 0 && I[k] % 32 == 0,
+                     "octsam_wgrad_tok_group: problem %d: M=%lld O=%d I=%d (O, I multiples of 32)", k,
+                     (long long)M[k], O[k], I[k]);
+    OCTSAM_CHECK_ARG(ldy[k] >= O[k] && ldx[k] >= I[k] && ldy[k] % 8 == 0 && ldx[k] % 8 == 0 &&
+                         ((uintptr_t)dy[k] & 15) == 0 && ((uintptr_t)x[k] & 15) == 0 &&
+                         (long long)M[k] * ldy[k] * 2 < (1LL << 31) && (long long)M[k] * ldx[k] * 2 < (1LL << 31),
+                     "octsam_wgrad_tok_group: problem %d: ldy / ldx multiples of 8, operands 16-B aligned", k);
+    TokGroup& g = M[k] > 1024 ? g8 : g4;
+    g.p[g.n] = TokProb{(const bf16*)dy[k], (const bf16*)x[k], out[k], db[k], (long long)ldy[k], (long long)ldx[k],
+                       (long long)M[k], I[k] / 32, I[k], beta[k]};
+    g.start[g.n + 1] = g.start[g.n] + (O[k] / 32) * (I[k] / 32);
+    ++g.n;
+  }
+  if (g8.n) launch_tok_group<8>(g8, (hipStream_t)stream);
+  OCTSAM_LAUNCH_CHECK("octsam_wgrad_tok_group");
+  if (g4.n) launch_tok_group<4>(g4, (hipStream_t)stream);
+  OCTSAM_LAUNCH_CHECK("octsam_wgrad_tok_group");
   return 0;
 }
 

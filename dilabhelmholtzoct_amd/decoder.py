@@ -294,6 +294,43 @@ class MaskDecoder(nn.Module):
     # octsam_upmask_bwd writes d up1, octsam_layernorm_bwd reads it back; A/B, scripts/step_ab3.py)
     fused_ln_bwd = True
 
+    # the backward's token-side weight gradients (octsam_wgrad_tok, ~18 us each, latency-bound, 29 per vit-b step)
+    # deferred to the end of backward() and issued as grouped launches (octsam_wgrad_tok_group; False: one launch
+    # each). A problem whose output overlaps a pending one's flushes the group first (the x_add / positional
+    # accumulations), and so does an in-place write into a tensor a pending problem reads (_before_write: d s4, which
+    # each block's projection backward accumulates into once its out_proj backward has read it).
+    tok_group = True
+    _tok_pending = None
+
+    @staticmethod
+    def _span(t):
+        """Byte range a (possibly strided) view touches."""
+        n = 1 + sum((d - 1) * st for d, st in zip(t.shape, t.stride())) if t.numel() else 0
+        return t.data_ptr(), t.data_ptr() + n * t.element_size()
+
+    def _defer_tok(self, prob):
+        dy, x, out, db = prob[0], prob[1], prob[3], prob[7]
+        spans = [self._span(out)] + ([self._span(db)] if db is not None else [])
+        busy = self._tok_spans
+        if any(a < d and c < b for a, b in spans for c, d in busy) or len(self._tok_pending) == K.TOK_GROUP_MAX:
+            self._flush_tok()
+        self._tok_pending.append(prob)
+        self._tok_spans.extend(spans)
+        self._tok_reads.extend([self._span(dy), self._span(x)])
+
+    def _before_write(self, t):
+        """t is about to be written in place: the deferred products that read it run first."""
+        if self._tok_pending:
+            a, b = self._span(t)
+            if any(a < d and c < b for c, d in self._tok_reads):
+                self._flush_tok()
+
+    def _flush_tok(self):
+        if self._tok_pending:
+            K.wgrad_tok_group(self._tok_pending)
+        self._tok_pending = [] if self._tok_pending is not None else None
+        self._tok_spans, self._tok_reads = [], []
+
     @staticmethod
     def _pick_split(Mtok, O, I):
         """Split-K (splits, rows per split) for a weight gradient with Mtok reduction rows: enough (O x I tiles)
@@ -337,16 +374,26 @@ class MaskDecoder(nn.Module):
             self._dw(S, x_add, rows, out, ldy=O, ldx=ldx, accumulate=True)
             return out
         beta = 1.0 if accumulate else 0.0
+        tok = (split is None and self.tok_wgrad and M < 65536 and dbx is None and O % 32 == 0 and I % 32 == 0
+               and ldy % 8 == 0 and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0
+               and out.is_contiguous())
+        if not tok and self._tok_pending:
+            # an immediate product must not overtake a deferred one into the same gradient
+            spans = [self._span(t) for t in (out, db, dbx) if t is not None]
+            if any(a < d and c < b for a, b in spans for c, d in self._tok_spans):
+                self._flush_tok()
         if (split is None and self.wide_wgrad and M >= 65536 and K.wgrad_supported(M, O, I) and ldy % 8 == 0
                 and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and out.is_contiguous()):
             # image side: one workgroup per CU holds the whole O x I output and streams its rows (octsam_wgrad)
             K.wgrad(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db, dbx=dbx, dbx_fold=dbx_fold)
             return out
-        if (split is None and self.tok_wgrad and M < 65536 and dbx is None and O % 32 == 0 and I % 32 == 0 and ldy % 8 == 0
-                and ldx % 8 == 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and out.is_contiguous()):
+        if tok:
             # token side (and image-side products over fewer rows): weight and bias gradient in one launch
-            # (octsam_wgrad_tok)
-            K.wgrad_tok(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db)
+            # (octsam_wgrad_tok); inside backward() deferred and issued in groups (octsam_wgrad_tok_group)
+            if self._tok_pending is not None:
+                self._defer_tok((dy, x, M, out, ldy, ldx, beta, db))
+            else:
+                K.wgrad_tok(dy, x, M, out, ldy=ldy, ldx=ldx, beta=beta, db=db)
             return out
         if split is None:
             split, Ks = self._pick_split(M, O, I)
@@ -631,6 +678,18 @@ class MaskDecoder(nn.Module):
 
     # ------------------------------------------------------------------ backward
     def backward_impl(self, s, dmasks):
+        """The decoder backward (every parameter gradient into the flat buffer G); with tok_group the token-side
+        weight gradients are deferred and issued in grouped launches before it returns."""
+        self._tok_pending = [] if self.tok_group and self.tok_wgrad else None
+        self._tok_spans, self._tok_reads = [], []
+        try:
+            G = self._backward_impl(s, dmasks)
+            self._flush_tok()
+        finally:
+            self._tok_pending = None
+        return G
+
+    def _backward_impl(self, s, dmasks):
         cfg = self.config
         B, N, T, P, R, L, RL = s.B, s.N, s.T, s.P, s.R, s.L, s.RL
         dev = dmasks.device
@@ -795,6 +854,7 @@ class MaskDecoder(nn.Module):
                 self._dw(dV_img, s.imgd_b, Mi, self.G(t2i + "v_proj.weight"), ldy=ldkv, db=self.G(t2i + "v_proj.bias"))
             else:
                 wg = self._group(self.flat_b16, kq + [t2i + "v_proj.weight"], C)
+                self._before_write(dkeys_in)  # (d s4, read by the deferred out_proj weight gradient at small RL)
                 self._dx(dKQV, wg, RL, dkeys_in, beta=1.0)
                 self._dw_pe(dKQV, ls.kv_src_b, RL, self._group(self.flat_grad, kq + [t2i + "v_proj.weight"], C),
                             2 * CI, s.pe_b, db=self._group(self.flat_grad, [t2i + "k_proj.bias", i2t + "q_proj.bias",

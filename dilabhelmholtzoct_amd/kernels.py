@@ -135,6 +135,34 @@ def wgrad_tok(dy: torch.Tensor, x: torch.Tensor, M: int, out: torch.Tensor, *, l
     return out
 
 
+TOK_GROUP_MAX = 24
+
+
+def wgrad_tok_group(problems) -> None:
+    """Several wgrad_tok problems in one launch (octsam_wgrad_tok_group): problems = [(dy, x, M, out, ldy, ldx, beta,
+    db)], at most TOK_GROUP_MAX, no two sharing an output; each gives the same bits as its own wgrad_tok call."""
+    n = len(problems)
+    if not 0 < n <= TOK_GROUP_MAX:
+        raise ValueError(f"wgrad_tok_group: 1..{TOK_GROUP_MAX} problems, got {n}")
+    arrs = {k: (t * n)() for k, t in (("dy", ctypes.c_void_p), ("x", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                                       ("db", ctypes.c_void_p), ("ldy", ctypes.c_int64), ("ldx", ctypes.c_int64),
+                                       ("M", ctypes.c_int64), ("O", ctypes.c_int32), ("I", ctypes.c_int32),
+                                       ("beta", ctypes.c_float))}
+    for k, (dy, x, M, out, ldy, ldx, beta, db) in enumerate(problems):
+        _require_cuda(dy, x, out, db)
+        if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("wgrad_tok_group: bf16 operands and contiguous fp32 outputs")
+        if db is not None and (db.dtype != torch.float32 or not db.is_contiguous()):
+            raise ValueError("wgrad_tok_group: db must be contiguous fp32")
+        O, I = out.shape
+        arrs["dy"][k], arrs["x"][k], arrs["out"][k], arrs["db"][k] = ptr(dy), ptr(x), ptr(out), ptr(db)
+        arrs["ldy"][k], arrs["ldx"][k], arrs["M"][k] = O if ldy is None else ldy, I if ldx is None else ldx, M
+        arrs["O"][k], arrs["I"][k], arrs["beta"][k] = O, I, beta
+    a = {k: ctypes.cast(v, ctypes.c_void_p) for k, v in arrs.items()}
+    _lib.call("octsam_wgrad_tok_group", n, a["dy"], a["ldy"], a["x"], a["ldx"], a["M"], a["O"], a["I"], a["out"],
+              a["beta"], a["db"])
+
+
 def ph_max_pairs(H: int, W: int) -> int:
     """Pair-buffer length that no [H, W] map can overflow: finite H0 pairs are born at regional minima
     (pairwise non-8-adjacent, <= ceil(H/2)*ceil(W/2)) and H1 pairs die at regional maxima (pairwise

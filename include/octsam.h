@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 21
+#define OCTSAM_ABI_VERSION 22
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -120,6 +120,12 @@ int32_t octsam_wgrad_supported(int64_t M, int32_t O, int32_t I);
  * deterministic). O, I multiples of 32; ldy, ldx multiples of 8; dy, x 16-B aligned. */
 int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I,
                      float* out, float beta, float* db, void* stream);
+/* n (1..24) independent octsam_wgrad_tok problems in ONE launch (ABI 22; host arrays of n entries each, db[k] may be
+ * NULL): the decoder backward defers its token-side weight gradients and issues them together. Problems of one call
+ * must not share an output (out / db); each keeps octsam_wgrad_tok's arithmetic (same bits). */
+int octsam_wgrad_tok_group(int32_t n, const void* const* dy, const int64_t* ldy, const void* const* x,
+                           const int64_t* ldx, const int64_t* M, const int32_t* O, const int32_t* I, float* const* out,
+                           const float* beta, float* const* db, void* stream);
 int64_t octsam_wgrad_workspace(int64_t M, int32_t O, int32_t I);
 int octsam_wgrad(const void* dy, int64_t ldy, const void* x, int64_t ldx, int64_t M, int32_t O, int32_t I, float* out,
                  float beta, float* db, float* dbx, int32_t dbx_fold, void* workspace, int64_t workspace_bytes,

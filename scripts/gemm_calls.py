@@ -55,7 +55,7 @@ def main():
     rows.sort(key=lambda r: -r[0])
     tot = sum(r[0] for r in rows)
     print(f"{len(rows)} gemm calls, {tot:.0f} us")
-    for r in rows[:40]:
+    for r in rows[:int(os.environ.get("TOP", "40"))]:
         print(f"{r[0]:8.1f} us  M={r[1]:7d} N={r[2]:5d} K={r[3]:6d} b={r[4]:3d} am={r[5]} bm={r[6]} out={r[7]:8s} "
               f"res={int(r[8])} act={r[9]} beta={r[10]} {r[11]:6.0f} TF/s")
 

@@ -9,7 +9,8 @@ tables, two workgroups per CU; n192 = octsam_gemm fast path 24 (256x192 tiles wh
 8-phase kernels otherwise); pp_unfused = the DiceCE backward and the post-processing row pass as two kernels with
 the [B, N, H, W] d-mask between them; t2isum_off = the first block's token->image backward per prompt +
 prompt group sums instead of octsam_dec_t2i_bwd_sum; dkeys_joint = the mask head's and the final attention's keys
-gradients as one product). Interleaved rounds, median of 5 rounds x 20 steps.
+gradients as one product; dkeys_two = the two-product form; tokgroup_off = every token-side weight gradient as its own
+launch instead of the deferred grouped launches). Interleaved rounds, median of 5 rounds x 20 steps.
 Diagnostic only."""
 import json
 import os
@@ -38,7 +39,8 @@ def main():
                 "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
                 "g4res_off": ({}, {}), "attn_v2": ({}, {}), "pp_unfused": ({"fused_pp": False}, {}),
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
-                "dkeys_joint": ({}, {"fuse_dkeys": True}), "g4w_off": ({}, {})}
+                "dkeys_joint": ({}, {"fuse_dkeys": True}), "dkeys_two": ({}, {"fuse_dkeys": False}),
+                "tokgroup_off": ({}, {"tok_group": False}), "g4w_off": ({}, {})}
     FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()

@@ -703,3 +703,31 @@ def test_gemm4w_conv3x3(cuda, C):
     ref = F.conv2d(x.permute(0, 3, 1, 2).float(), W.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
     for out, _ in outs:
         assert _rel(out, ref) < 1e-5
+
+
+def test_wgrad_tok_group_matches_single_launches(cuda):
+    """octsam_wgrad_tok_group (ABI 22): several token-side weight gradients in one launch -- the decoder backward's
+    deferred form -- give the same bits as one octsam_wgrad_tok launch each (strided dy, with and without bias
+    sums, beta 0 and 1, M on both sides of the single-launch kernel's 8-wave threshold)."""
+    from dilabhelmholtzoct_amd import kernels
+    g = torch.Generator().manual_seed(7)
+    probs, refs = [], []
+    for k, (M, O, I, ldy, db, beta) in enumerate([(1176, 256, 256, 256, True, 0.0), (1176, 128, 256, 384, True, 1.0),
+                                                  (700, 256, 2048, 256, False, 0.0), (4096, 256, 128, 512, True, 0.0),
+                                                  (147, 32, 64, 40, True, 0.0)]):
+        dy = (torch.randn(M, ldy, generator=g) * 0.1).to(cuda, torch.bfloat16)
+        x = torch.randn(M, I, generator=g).to(cuda, torch.bfloat16)
+        out0 = torch.randn(O, I, generator=g).to(cuda)
+        outs = [out0.clone(), out0.clone()]
+        dbs = [torch.empty(O, device=cuda), torch.empty(O, device=cuda)] if db else [None, None]
+        kernels.wgrad_tok(dy, x, M, outs[0], ldy=ldy, beta=beta, db=dbs[0])
+        probs.append((dy, x, M, outs[1], ldy, None, beta, dbs[1]))
+        refs.append((outs, dbs, dy, x, M, O, beta, out0))
+    kernels.wgrad_tok_group(probs)
+    torch.cuda.synchronize()
+    for outs, dbs, dy, x, M, O, beta, out0 in refs:
+        assert torch.equal(outs[0], outs[1])
+        if dbs[0] is not None:
+            assert torch.equal(dbs[0], dbs[1])
+        ref = dy[:, :O].float().t() @ x.float() + beta * out0
+        assert _rel(outs[1], ref) < 1e-5
