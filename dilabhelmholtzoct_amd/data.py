@@ -150,8 +150,9 @@ class SAMDataset(torch.utils.data.Dataset):
             seed_sample(self.epoch, idx, self.epoch_seed)
         item = self.dataset[idx]
         image = np.array(item["image"])
-        if self.config.get("pseudocolor") is not None:
-            raise NotImplementedError("cv2 pseudocolor maps are not available offline")
+        if self.config.get("pseudocolor") is not None:  # ref:octsam/models/training_utils.py:439-440
+            from .colormaps import apply_colormap, colormap_lut
+            image = apply_colormap(image, colormap_lut(self.config["pseudocolor"]))
         gt = np.array(item["label"])
         if self.config.get("prompt_type") == "points":
             return [image, *self.get_points_and_gt_masks(gt)]

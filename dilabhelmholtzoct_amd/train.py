@@ -674,10 +674,12 @@ def _prep(ds, idx, prompt, device, device_data):
     from . import data
     if device_data and idx:
         from .components import ComponentLimitError, collate_device_begin
-        if ds.config.get("pseudocolor") is not None:
-            raise NotImplementedError("cv2 pseudocolor maps are not available offline")
         its = [ds.dataset[i] for i in idx]
         imgs = np.stack([np.array(it["image"]) for it in its])
+        if ds.config.get("pseudocolor") is not None:  # as SAMDataset.__getitem__ (a host gather per pixel)
+            from .colormaps import apply_colormap, colormap_lut
+            lut = colormap_lut(ds.config["pseudocolor"])
+            imgs = np.stack([apply_colormap(im, lut) for im in imgs])
         if imgs.ndim == 3:  # grayscale scans: the processor's convert_rgb replicates the channel
             imgs = np.repeat(imgs[..., None], 3, -1)
         labs = np.stack([np.array(it["label"]) for it in its]).astype(np.uint8)
@@ -978,8 +980,11 @@ def main(argv=None):
     args = build_parser().parse_args(argv)
     if args.loss != "diceCE" or args.optimizer != "adam":
         raise SystemExit("only --loss diceCE and --optimizer adam exist in the reference")
-    if args.pseudocolor != "grayscale":
-        raise SystemExit("pseudocolour maps need cv2, which is not available")
+    from .colormaps import colormap_lut
+    try:  # the reference's OCV_COLORMAPS[args.pseudocolor] (ref:octsam/models/training.py:123)
+        pseudocolor = colormap_lut(args.pseudocolor)
+    except (KeyError, NotImplementedError) as e:
+        raise SystemExit(f"--pseudocolor: {e}")
     now = datetime.datetime.now().strftime("%y-%m-%d_%H.%M.%S")
     name = args.display_name or (f"{'{:.0e}'.format(args.lr)} lr,{'{:.0e}'.format(args.weight_decay)} wd,"
                                  f"{args.bs} bs, {args.loss} loss, {args.pseudocolor}, {now}")
@@ -989,7 +994,7 @@ def main(argv=None):
               "learning_rate": args.lr, "weight_decay": args.weight_decay, "epochs": args.epochs,
               "batch_size": args.bs, "shuffle": args.shuffle, "optimizer": args.optimizer, "loss": args.loss,
               "time": now, "evaluate": args.evaluate, "topological": args.top, "prompt_type": args.prompt,
-              "pseudocolor": None, "encoder_dtype": args.precision, "graphs": args.graphs, "pipeline": args.pipeline}
+              "pseudocolor": pseudocolor, "encoder_dtype": args.precision, "graphs": args.graphs, "pipeline": args.pipeline}
     pg = None
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
