@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--model", default="facebook/sam-vit-base")
     p.add_argument("--prompt", default="bboxes", choices=["bboxes", "points", "both"])
     p.add_argument("--top", type=int, default=1)
+    p.add_argument("--fork-topo", type=int, default=1,
+                   help="persistence + transport beside the DiceCE backward (FusedTrainStep.fork_topo; 0: A/B)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
                    help="16-bit operand type of the frozen encoder (fp16: BASELINE configs[4]); the decoder is bf16")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle step (rank 0, N=1)")
@@ -597,6 +599,7 @@ def main():
     pipe = bool(args.pipeline) and not args.eager
     step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager,
                           pipeline=pipe)
+    step.fork_topo = bool(args.fork_topo)
 
     def barrier():
         if pg is not None:

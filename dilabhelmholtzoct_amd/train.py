@@ -90,11 +90,13 @@ class FusedTrainStep:
         self.pipeline_sets = 2
         self._prefetch = None   # (encoder set, pixel tag) whose E was replayed ahead on the encoder stream
         self._w2_stream = None  # side stream of the device topological forward (forked in F2, joined before B)
-        # w2 = "device": only the transport forks beside the DiceCE backward, the resampling + persistence run in F
-        # (True: those forked too; same-process A/B, scripts/step_ab3.py, profiles/r03/step_ab_fork_tokdw.log:
-        # 17.04 vs 17.13 ms/step — the 16-workgroup persistence kernel beside the DiceCE backward delays it more
-        # than it gains)
-        self.fork_topo = False
+        # w2 = "device": the 50x50 resampling, the persistence and the transport fork beside the DiceCE backward
+        # (False: only the transport, the resampling + persistence in F). Same-process A/B (scripts/step_ab3.py):
+        # round 3 measured the fork slower (profiles/r03/step_ab_fork_tokdw.log, 17.04 vs 17.13 ms/step); with the
+        # fused DiceCE / post-processing row pass of round 4 it is faster, 16.31 -> 16.16 ms pipelined and 18.77 ->
+        # 18.55 sequential (profiles/r05/fork_topo_ab.log): the 16-workgroup persistence kernel (348 us) no longer
+        # runs alone on the main stream
+        self.fork_topo = True
         # DiceCE backward fused with the post-processing adjoint's row pass (no [B, N, H, W] d-mask round trip;
         # False: the round-3 octsam_dicece_bwd + octsam_postproc_bwd path, for A/B)
         self.fused_pp = True

@@ -2,7 +2,7 @@
 --top=True) for variants of the step / mask decoder set while the graphs are captured (STEP_VARIANTS: default,
 wgrad_off = image-side weight gradients by the split-K tile GEMM, tok_off = token-side ones by the split-K tile
 GEMM + reductions + column-sum kernels, fork_topo = resampling + persistence forked beside
-the DiceCE backward too, ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
+the DiceCE backward too (the default since round 5; topo_in_f = not forked), ln_sep = the upscaling LayerNorm2d + GELU backward as its own kernel instead of fused into
 the mask-head backward, g4res_off = the decoder's [K | Q' | V] projection on the persistent 8-phase GEMM in plain tile
 order, octsam_gemm fast path 1 | 1024 | 2048, while capturing; attn_v2 = the global attention with whole rel_h
 tables, two workgroups per CU; n192 = octsam_gemm fast path 24 (256x192 tiles where they fill the waves better, the
@@ -36,7 +36,7 @@ def main():
     dec = model.mask_decoder
     # (name, attributes of the step, attributes of the mask decoder read while the graphs are captured)
     VARIANTS = {"default": ({}, {}), "wgrad_off": ({}, {"wide_wgrad": False}), "tok_off": ({}, {"tok_wgrad": False}),
-                "fork_topo": ({"fork_topo": True}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
+                "fork_topo": ({"fork_topo": True}, {}), "topo_in_f": ({"fork_topo": False}, {}), "ln_sep": ({}, {"fused_ln_bwd": False}),
                 "g4res_off": ({}, {}), "attn_v2": ({}, {}), "pp_unfused": ({"fused_pp": False}, {}),
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
                 "dkeys_joint": ({}, {"fuse_dkeys": True}), "dkeys_two": ({}, {"fuse_dkeys": False}),

@@ -35,11 +35,12 @@ def test_graph_step_matches_eager(cuda, top):
         assert float(lg[-1][2]) > 0.0
 
 
-@pytest.mark.parametrize("variant", ["fork_topo", "w2_host"])
+@pytest.mark.parametrize("variant", ["topo_in_f", "w2_host"])
 def test_graph_step_topo_variants_match_default(cuda, variant):
-    """The A/B arrangements of the topological forward inside the graphs — resampling + persistence forked beside the
-    DiceCE backward too (fork_topo), the transport on the host between F and B (w2="host") — give the same losses and
-    updated weights as the default graph step (the same kernels; host W2 is bit-identical to the device one)."""
+    """The A/B arrangements of the topological forward inside the graphs — resampling + persistence in F with only the
+    transport forked beside the DiceCE backward (fork_topo = False; the default forks all three), the transport on
+    the host between F and B (w2="host") — give the same losses and updated weights as the default graph step (the
+    same kernels; host W2 is bit-identical to the device one)."""
     from dilabhelmholtzoct_amd.model import SamModel
     from dilabhelmholtzoct_amd.train import FusedTrainStep
     batch = _batch(cuda)
@@ -47,7 +48,8 @@ def test_graph_step_topo_variants_match_default(cuda, variant):
     for v in ("default", variant):
         model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(cuda)
         step = FusedTrainStep(model, topological=True, graphs=True, w2="host" if v == "w2_host" else "device")
-        step.fork_topo = v == "fork_topo"
+        if v == "topo_in_f":
+            step.fork_topo = False
         losses = [step.step(batch).clone() for _ in range(3)]
         step.flush()
         torch.cuda.synchronize()
