@@ -111,6 +111,7 @@ class GemmEventTimer:
         self.events = []
         self.flops = 0.0
         self.bytes = 0.0
+        self.lib_events = []
 
     def __enter__(self):
         orig = self.orig
@@ -125,7 +126,10 @@ class GemmEventTimer:
                 s.record()
                 out = orig(A, B, **kw)
                 e.record()
-                if lib.octsam_gemm_last_path() == 2:
+                path = lib.octsam_gemm_last_path()
+                if path == 5:  # hipBLASLt (encoder MLP2 / projection): reported beside the family, not in it
+                    self.lib_events.append((s, e, 2.0 * kw["M"] * kw["N"] * kw["K"]))
+                if path == 2:
                     fl = 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
                     # compulsory bytes: A, B read once, C written once (+ residual read), per launch
                     bt = kw.get("batch", 1)
@@ -155,6 +159,18 @@ class GemmEventTimer:
         ms = sum(s.elapsed_time(e) for s, e, _, _ in self.events)
         n = len(self.events)
         return ms, n, self.flops
+
+    def library(self):
+        """The GEMMs octsam_gemm hands to hipBLASLt (path 5: the encoder's in-place-residual MLP2 / projection)."""
+        if not self.lib_events:
+            return None
+        ms = sum(s.elapsed_time(e) for s, e, _ in self.lib_events)
+        fl = sum(f for _, _, f in self.lib_events)
+        a = fl / (ms * 1e-3) / 1e12
+        return {"kernel": "hipBLASLt (octsam_gemm path 5: encoder MLP2 + attention projection, x += A W^T + b on "
+                          "the fp32 residual stream)", "bound": "mfma", "achieved": round(a, 2),
+                "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(a / MI355X_BF16_DENSE_TFLOPS, 4),
+                "launches": len(self.lib_events), "avg_launch_us": round(ms * 1e3 / len(self.lib_events), 2)}
 
     def by_bound(self):
         """The family's launches split by their compulsory arithmetic intensity against the MI355X ridge
@@ -724,6 +740,7 @@ def main():
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}
             roof["family_by_intensity"] = timer.by_bound()
+            roof["library_gemm"] = timer.library()
             roof.update(split)
 
     e2e = None

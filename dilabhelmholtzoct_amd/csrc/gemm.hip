@@ -2518,6 +2518,11 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 
 }  // namespace
 
+// hipBLASLt for the plain in-place-residual encoder GEMMs (blaslt.cpp)
+bool blaslt_eligible(const octsam_gemm_args* a);
+int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s, bool f16);
+extern int g_blaslt_enabled;
+
 // launch options and the last path taken are shared by the bf16 and fp16 builds of this file (the bf16
 // build owns them; the fp16 build reaches them through these hidden accessors), so
 // octsam_gemm_set_fast_path / octsam_gemm_last_path cover both entry points
@@ -2543,6 +2548,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_gemm4w_res = (enable & 1024) ? 0 : 1;
   g_rgroup = (enable & 2048) ? 0 : 1;
   g_res_lds = (enable & 4096) ? 0 : 1;
+  g_blaslt_enabled = (enable & 65536) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2576,6 +2582,17 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   if (a->a_mode == 3)
     OCTSAM_CHECK_ARG(a->conv_c % 8 == 0 && a->K == 9 * a->conv_c && a->M % 4096 == 0,
                      "octsam_gemm: conv3x3 mode needs K=9*C, C%%8==0, M=B*4096");
+  if (g_use_glds == 1 && blaslt_eligible(a)) {
+#ifdef OCTSAM_GEMM_F16
+    const int r = blaslt_gemm(a, (hipStream_t)stream, true);
+#else
+    const int r = blaslt_gemm(a, (hipStream_t)stream, false);
+#endif
+    if (r != 0) {
+      t_last_path = 5;
+      return r < 0 ? 1 : 0;
+    }
+  }
   GemmK k;
   k.A2 = a->A2; k.B2 = a->B2; k.a2_rows = a->a2_rows; k.b2_rows = a->b2_rows;
   k.a_blk = a->a_blk; k.a_rep = a->a_rep > 0 ? a->a_rep : 1;

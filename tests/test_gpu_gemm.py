@@ -310,7 +310,7 @@ def test_gemm8_n192_tiles(cuda, M, N, K, kind, act):
     X0 = torch.randn(M, N, generator=g).to(cuda, torch.float32 if f32 else torch.bfloat16)
     outs = []
     for fast in (24, 1):  # 24: 256x192 tiles where they quantise better; 1: the default 256x256 tiles
-        lib.octsam_gemm_set_fast_path(fast | 256)
+        lib.octsam_gemm_set_fast_path(fast | 256 | 65536)  # (65536: the in-place residual kind stays native)
         out = X0.clone()
         kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, act=act, residual=out if f32 else None)
         assert lib.octsam_gemm_last_path() == 2
@@ -437,6 +437,39 @@ def test_gemm_small_path(cuda, a_mode, b_mode, shape):
     assert lib.octsam_gemm_last_path() == 3
     ref = F.relu(torch.bmm(A.float(), W.float().transpose(1, 2)).to(cuda) + bias) + R
     assert _rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,f16,bias", [(32768, 768, 3072, False, True), (32768, 768, 768, False, True),
+                                           (16384, 1280, 5120, True, True), (24576, 256, 512, False, False)])
+def test_gemm_blaslt_inplace_residual(cuda, M, N, K, f16, bias):
+    """The in-place fp32 residual GEMM x += A W^T + b (the encoder's MLP2 / projection) on the hipBLASLt path (path
+    5, default): against torch fp32, bit-identical run to run, within 1e-5 of the native 8-phase kernels (fast path
+    bit 65536); and the same call on a shape outside the path's range stays native."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    e16 = torch.float16 if f16 else torch.bfloat16
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(cuda, e16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, e16)
+    b = torch.randn(N, generator=g).to(cuda) if bias else None
+    X0 = torch.randn(M, N, generator=g).to(cuda)
+    outs = []
+    for fast in (1, 1, 1 | 65536):
+        lib.octsam_gemm_set_fast_path(fast)
+        x = X0.clone()
+        kernels.gemm(A, W, M=M, N=N, K=K, out=x, bias=b, residual=x)
+        assert lib.octsam_gemm_last_path() == (5 if fast == 1 else 2)
+        outs.append(x)
+    lib.octsam_gemm_set_fast_path(1)
+    ref = A.float() @ W.float().t() + (b if bias else 0.0) + X0
+    assert _rel(outs[0], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+    assert _rel(outs[0], outs[2]) < 1e-5
+    x = X0[:4096].clone()
+    lib.octsam_gemm_set_fast_path(1 | 256)  # (256: not the small-problem kernel either)
+    kernels.gemm(A[:4096], W, M=4096, N=N, K=K, out=x, bias=b, residual=x)
+    assert lib.octsam_gemm_last_path() == 2
+    lib.octsam_gemm_set_fast_path(1)
 
 
 def test_gemm_small_path_ktotal(cuda):
