@@ -64,7 +64,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
         c_rows=_mapped_rows(out, ldc, residual, ldr, pre_out) if row_map is not None else 0,
         a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
-    if residual is not None and residual.data_ptr() == out.data_ptr():
+    if M >= 8192:  # (the sizes octsam_gemm may hand to hipBLASLt)
         _gemm_workspace(out.device)
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
@@ -75,8 +75,8 @@ _GEMM_WS = {}  # device index -> workspace tensor handed to octsam_gemm_set_work
 
 
 def _gemm_workspace(dev: torch.device):
-    """The hipBLASLt path's workspace on dev (octsam_gemm_set_workspace), allocated on the first in-place-residual
-    GEMM of the process (the eager pass before any graph capture; never from inside a capture)."""
+    """The hipBLASLt path's workspace on dev (octsam_gemm_set_workspace), allocated on the first large GEMM of the
+    process (the eager pass before any graph capture; never from inside a capture)."""
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     if idx in _GEMM_WS or torch.cuda.is_current_stream_capturing():
         return

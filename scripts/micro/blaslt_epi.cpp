@@ -60,8 +60,21 @@ int main() {
   void* ws;
   CK(hipMalloc(&ws, ws_bytes));
   Shape shapes[] = {{"fc2", 32768, 768, 3072, true}, {"qkv", 32768, 2304, 768, false},
-                    {"proj", 32768, 768, 768, true}, {"fc1_bias_only", 32768, 3072, 768, false}};
+                    {"proj", 32768, 768, 768, true}, {"fc1_bias_only", 32768, 3072, 768, false},
+                    {"dec_256x512", 688128, 256, 512, false}, {"dec_256x256", 688128, 256, 256, false},
+                    {"dec_128x256", 688128, 128, 256, false}, {"dec_384x256", 688128, 384, 256, false}};
+  const char* only = std::getenv("SHAPES");
   for (const Shape& s : shapes) {
+    if (only) {  // SHAPES: comma list of name prefixes
+      bool hit = false;
+      for (const char* t = only; *t;) {
+        const char* e = std::strchr(t, ',');
+        const size_t n = e ? (size_t)(e - t) : std::strlen(t);
+        if (n && std::strncmp(s.name, t, n) == 0) hit = true;
+        t += n + (e ? 1 : 0);
+      }
+      if (!hit) continue;
+    }
     const long long nA = (long long)s.M * s.K, nW = (long long)s.N * s.K, nD = (long long)s.M * s.N;
     uint16_t *A, *W;
     float* bias;
