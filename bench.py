@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--model", default="facebook/sam-vit-base")
     p.add_argument("--prompt", default="bboxes", choices=["bboxes", "points", "both"])
     p.add_argument("--top", type=int, default=1)
+    p.add_argument("--gemm-fast-path", type=int, default=1,
+                   help="octsam_gemm_set_fast_path value for the run (1: default; A/B only)")
     p.add_argument("--fork-topo", type=int, default=1,
                    help="persistence + transport beside the DiceCE backward (FusedTrainStep.fork_topo; 0: A/B)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
@@ -616,6 +618,9 @@ def main():
     step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager,
                           pipeline=pipe)
     step.fork_topo = bool(args.fork_topo)
+    if args.gemm_fast_path != 1:  # (A/B of octsam_gemm's paths, e.g. 65537: no hipBLASLt)
+        from dilabhelmholtzoct_amd import _lib
+        _lib.load().octsam_gemm_set_fast_path(args.gemm_fast_path)
 
     def barrier():
         if pg is not None:

@@ -95,8 +95,9 @@ int octsam_gemm_f16(const octsam_gemm_args* args, void* stream);
    hipBLASLt path */
 void octsam_gemm_set_fast_path(int32_t enable);
 /* Workspace (device memory owned by the caller, current device) for octsam_gemm's hipBLASLt path: the plain
-   in-place-residual GEMM x += A W^T (+ bias) with x fp32 (R == C), K-contiguous operands, one batch, no activation,
-   M >= 8192, N >= 256, K >= 512 -- the ViT encoder's MLP2 and attention projection (replaces the same
+   in-place-residual GEMM x += A W^T (+ bias) with x fp32 (R == C), bf16 K-contiguous operands (octsam_gemm; the
+   fp16 octsam_gemm_f16 stays native), one batch, no activation, M >= 8192, N >= 256, K >= 512 -- the ViT encoder's
+   MLP2 and attention projection (replaces the same
    octsam_gemm call; hf:modeling_sam.py SamVisionLayer.forward residual adds). Without a workspace (or bytes = 0)
    those GEMMs run on the native kernels. ABI 23. */
 int octsam_gemm_set_workspace(void* workspace, int64_t bytes);

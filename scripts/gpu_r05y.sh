@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: vit-l bf16 (configs[3] slice, points, B = 4) with and without the hipBLASLt path, alternating processes on one box.
+set -u
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${TAG:-r05y}; mkdir -p $O; cd $R
+timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_gemm.py -k "blaslt or n192" > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+F="--model facebook/sam-vit-large --prompt points --batch 4 --cpu-baseline 0 --val 0 --val-protocol 0 --data-path 0 --e2e-steps 0 --topo-all 0 --loop-images 0 --top-off 0 --roof-steps 0"
+for rnd in 1 2; do
+  for fp in 1 65537; do
+    timeout -k 10 400 python bench.py $F --gemm-fast-path $fp > $O/b_${fp}_$rnd.json 2> $O/b_${fp}_$rnd.err || { tail -5 $O/b_${fp}_$rnd.err; exit 1; }
+    python -c "import json; d=json.loads(open('$O/b_${fp}_$rnd.json').read().strip().splitlines()[-1]); print('fast_path=$fp round $rnd', d['value'], d['ms_per_step'], d.get('sequential_ms_per_step'))"
+  done
+done

@@ -439,18 +439,18 @@ def test_gemm_small_path(cuda, a_mode, b_mode, shape):
     assert _rel(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K,f16,bias", [(32768, 768, 3072, False, True), (32768, 768, 768, False, True),
-                                           (16384, 1280, 5120, True, True), (24576, 256, 512, False, False)])
-def test_gemm_blaslt_inplace_residual(cuda, M, N, K, f16, bias):
-    """The in-place fp32 residual GEMM x += A W^T + b (the encoder's MLP2 / projection) on the hipBLASLt path (path
-    5, default): against torch fp32, bit-identical run to run, within 1e-5 of the native 8-phase kernels (fast path
-    bit 65536); and the same call on a shape outside the path's range stays native."""
+@pytest.mark.parametrize("M,N,K,bias", [(32768, 768, 3072, True), (32768, 768, 768, True), (16384, 1024, 4096, True),
+                                      (24576, 256, 512, False)])
+def test_gemm_blaslt_inplace_residual(cuda, M, N, K, bias):
+    """The in-place fp32 residual GEMM x += A W^T + b (the bf16 encoder's MLP2 / projection: vit-b, vit-l) on the
+    hipBLASLt path (path 5, default): against torch fp32, bit-identical run to run, within 1e-5 of the native 8-phase
+    kernels (fast path bit 65536); the same call on a shape outside the path's range, and the fp16 encoder's
+    (octsam_gemm_f16), stay native."""
     from dilabhelmholtzoct_amd import _lib, kernels
     lib = _lib.load()
-    e16 = torch.float16 if f16 else torch.bfloat16
     g = torch.Generator().manual_seed(M + N + K)
-    A = torch.randn(M, K, generator=g).to(cuda, e16)
-    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, e16)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
     b = torch.randn(N, generator=g).to(cuda) if bias else None
     X0 = torch.randn(M, N, generator=g).to(cuda)
     outs = []
@@ -470,6 +470,9 @@ def test_gemm_blaslt_inplace_residual(cuda, M, N, K, f16, bias):
     kernels.gemm(A[:4096], W, M=4096, N=N, K=K, out=x, bias=b, residual=x)
     assert lib.octsam_gemm_last_path() == 2
     lib.octsam_gemm_set_fast_path(1)
+    x = X0.clone()
+    kernels.gemm(A.half(), W.half(), M=M, N=N, K=K, out=x, bias=b, residual=x)
+    assert lib.octsam_gemm_last_path() == 2
 
 
 def test_gemm_small_path_ktotal(cuda):
