@@ -1,4 +1,5 @@
-// hipBLASLt for the plain in-place-residual encoder GEMMs (library GEMM; the hand-written kernels keep the rest).
+// hipBLASLt for the encoder's plain GEMMs: the in-place-residual MLP2 / projection and the QKV projection (library
+// GEMMs; the hand-written kernels keep the rest).
 //
 // The encoder's MLP2 and attention projection are x += A W^T + b on the fp32 residual stream x (hf:modeling_sam.py
 // SamVisionLayer: hidden_states = residual + mlp(...) / + attn(...)): a plain GEMM with a bias epilogue and beta = 1
@@ -37,8 +38,8 @@ struct Dev {
   hipblasLtHandle_t h = nullptr;
   void* ws = nullptr;
   size_t ws_bytes = 0;
-  // (M, N, K, f16 operands, bias)
-  std::map<std::tuple<int, int, int, int, int>, Plan> plans;
+  // (M, N, K, f16 operands, bias, 16-bit D)
+  std::map<std::tuple<int, int, int, int, int, int>, Plan> plans;
 };
 std::mutex g_mu;
 std::map<int, Dev> g_devs;
@@ -58,7 +59,7 @@ bool make_plan(Dev& d, const octsam_gemm_args* a, bool f16, Plan& p) {
   }
   if (hipblasLtMatrixLayoutCreate(&p.la, et, a->K, a->N, a->K) != HIPBLAS_STATUS_SUCCESS ||
       hipblasLtMatrixLayoutCreate(&p.lb, et, a->K, a->M, a->K) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, a->N, a->M, a->N) != HIPBLAS_STATUS_SUCCESS)
+      hipblasLtMatrixLayoutCreate(&p.lc, a->c_f32 ? HIP_R_32F : et, a->N, a->M, a->N) != HIPBLAS_STATUS_SUCCESS)
     return false;
   hipblasLtMatmulPreference_t pref;
   if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return false;
@@ -75,15 +76,22 @@ bool make_plan(Dev& d, const octsam_gemm_args* a, bool f16, Plan& p) {
 }  // namespace
 
 int g_blaslt_enabled = 1;  // octsam_gemm_set_fast_path bit 65536 turns it off (A/B)
+int g_blaslt_qkv = 1;      // bit 131072 turns the QKV kind off (A/B)
 
-// Eligible: x += A W^T (+ bias) with x fp32 and the residual IS the output (in place), K-contiguous dense
-// operands, one batch, no activation / scaling / row map; large M (the encoder's token rows).
+// Eligible, with K-contiguous dense operands, one batch, no activation / scaling / row map, M >= 8192 (the encoder's
+// token rows), either
+//   x += A W^T (+ bias) with x fp32 and the residual IS the output (in place), N >= 256, K >= 512: MLP2, projection;
+//   or a 16-bit D = A W^T + bias, no residual, 2048 <= N <= 4096, K <= 1024: the QKV projection (same-process step
+//   A/B 16.28 -> 15.92 ms pipelined, 18.16 -> 17.99 sequential, profiles/r05/blaslt_step_ab.log).
+// (MLP1 has the GELU: native. The decoder's plain 16-bit image-side products measured slower in the step.)
 bool blaslt_eligible(const octsam_gemm_args* a) {
-  return g_blaslt_enabled && a->batch == 1 && a->a_mode == 0 && a->b_mode == 0 && !a->row_map && !a->C_pre &&
-         !a->A2 && !a->B2 && !a->a_blk && !a->b_blk && !a->r_blk && !a->k_total && !a->a_colsum && !a->b_colsum &&
-         a->act == 0 && a->alpha == 1.0f && a->beta == 0.0f && a->c_f32 && a->r_f32 && a->R == a->C &&
-         a->ldr == a->ldc && a->lda == a->K && a->ldb == a->K && a->ldc == a->N && a->M >= 8192 && a->N >= 256 &&
-         a->K >= 512;
+  if (!(g_blaslt_enabled && a->batch == 1 && a->a_mode == 0 && a->b_mode == 0 && !a->row_map && !a->C_pre &&
+        !a->A2 && !a->B2 && !a->a_blk && !a->b_blk && !a->r_blk && !a->k_total && !a->a_colsum && !a->b_colsum &&
+        a->act == 0 && a->alpha == 1.0f && a->beta == 0.0f && a->lda == a->K && a->ldb == a->K && a->ldc == a->N &&
+        a->M >= 8192))
+    return false;
+  if (!a->c_f32) return g_blaslt_qkv && a->R == nullptr && a->bias && a->N >= 2048 && a->N <= 4096 && a->K <= 1024;
+  return a->r_f32 && a->R == a->C && a->ldr == a->ldc && a->N >= 256 && a->K >= 512;
 }
 
 // 1: ran, 0: not taken (no workspace, no plan: the caller runs the native kernels), -1: error (set)
@@ -97,7 +105,7 @@ int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s, bool f16) {
     d.h = nullptr;
     return 0;
   }
-  const auto key = std::make_tuple(a->M, a->N, a->K, f16 ? 1 : 0, a->bias ? 1 : 0);
+  const auto key = std::make_tuple(a->M, a->N, a->K, f16 ? 1 : 0, a->bias ? 1 : 0, a->c_f32 ? 0 : 1);
   auto it = d.plans.find(key);
   if (it == d.plans.end()) {
     Plan p;
@@ -107,7 +115,7 @@ int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s, bool f16) {
   Plan& p = it->second;
   if (!p.ok) return 0;
   if (a->bias) hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a->bias, sizeof(a->bias));
-  const float alpha = 1.0f, beta = 1.0f;
+  const float alpha = 1.0f, beta = a->c_f32 ? 1.0f : 0.0f;  // (fp32: the in-place residual)
   const hipblasStatus_t st = hipblasLtMatmul(d.h, p.desc, &alpha, a->B, p.la, a->A, p.lb, &beta, a->C, p.lc, a->C,
                                              p.lc, &p.algo, d.ws, d.ws_bytes, s);
   if (st != HIPBLAS_STATUS_SUCCESS) {

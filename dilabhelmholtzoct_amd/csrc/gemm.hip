@@ -2522,6 +2522,7 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 bool blaslt_eligible(const octsam_gemm_args* a);
 int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s, bool f16);
 extern int g_blaslt_enabled;
+extern int g_blaslt_qkv;
 
 // launch options and the last path taken are shared by the bf16 and fp16 builds of this file (the bf16
 // build owns them; the fp16 build reaches them through these hidden accessors), so
@@ -2549,6 +2550,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_rgroup = (enable & 2048) ? 0 : 1;
   g_res_lds = (enable & 4096) ? 0 : 1;
   g_blaslt_enabled = (enable & 65536) ? 0 : 1;
+  g_blaslt_qkv = (enable & 131072) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }

@@ -475,6 +475,34 @@ def test_gemm_blaslt_inplace_residual(cuda, M, N, K, bias):
     assert lib.octsam_gemm_last_path() == 2
 
 
+@pytest.mark.parametrize("M,N,K", [(32768, 2304, 768), (16384, 3072, 1024)])
+def test_gemm_blaslt_qkv(cuda, M, N, K):
+    """The QKV kind on the hipBLASLt path (bf16 D = A W^T + b, vit-b / vit-l shapes): against torch fp32,
+    bit-identical run to run, within bf16 rounding of the native kernels (fast path bit 131072); with an activation
+    (MLP1) the call stays native."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(cuda)
+    outs = []
+    for fast in (1, 1, 1 | 131072):
+        lib.octsam_gemm_set_fast_path(fast)
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=b)
+        assert lib.octsam_gemm_last_path() == (5 if fast == 1 else 2)
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    ref = A.float() @ W.float().t() + b
+    assert _rel(outs[0], ref) < 8e-3
+    assert torch.equal(outs[0], outs[1])
+    assert _rel(outs[0], outs[2]) < 8e-3
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=b, act=2)
+    assert lib.octsam_gemm_last_path() == 2
+
+
 def test_gemm_small_path_ktotal(cuda):
     """Split-K with a ragged total (k_total): rows past k_total read as zero on the small-problem path."""
     from dilabhelmholtzoct_amd import _lib, kernels
