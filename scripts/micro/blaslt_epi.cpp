@@ -49,6 +49,7 @@ struct Shape {
   const char* name;
   int M, N, K;
   bool f32_inplace;  // fp32 D += A W^T + bias; else bf16 D = A W^T + bias
+  int gelu = 0;      // 1: bf16 D = GELU(A W^T + bias) (hipBLASLt's GELU epilogue against octsam's exact-erf GELU)
 };
 
 int main() {
@@ -62,7 +63,8 @@ int main() {
   Shape shapes[] = {{"fc2", 32768, 768, 3072, true}, {"qkv", 32768, 2304, 768, false},
                     {"proj", 32768, 768, 768, true}, {"fc1_bias_only", 32768, 3072, 768, false},
                     {"dec_256x512", 688128, 256, 512, false}, {"dec_256x256", 688128, 256, 256, false},
-                    {"dec_128x256", 688128, 128, 256, false}, {"dec_384x256", 688128, 384, 256, false}};
+                    {"dec_128x256", 688128, 128, 256, false}, {"dec_384x256", 688128, 384, 256, false},
+                    {"fc1_gelu", 32768, 3072, 768, false, 1}};
   const char* only = std::getenv("SHAPES");
   for (const Shape& s : shapes) {
     if (only) {  // SHAPES: comma list of name prefixes
@@ -98,7 +100,7 @@ int main() {
     hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
-    hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+    hipblasLtEpilogue_t epi = s.gelu ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_BIAS;
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
     CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
     hipDataType bt = HIP_R_32F;
@@ -124,6 +126,7 @@ int main() {
     g.M = s.M; g.N = s.N; g.K = s.K; g.batch = 1;
     g.lda = s.K; g.ldb = s.K; g.ldc = s.N; g.ldr = s.N;
     g.alpha = 1.0f; g.beta = 0.0f; g.c_f32 = s.f32_inplace; g.r_f32 = s.f32_inplace;
+    g.act = s.gelu ? OCTSAM_ACT_GELU : 0;
     auto run_ours = [&]() {
       if (s.f32_inplace) CK(hipMemcpyAsync(Dref, D0, nD * es, hipMemcpyDeviceToDevice, st));
       CK(octsam_gemm(&g, st));
