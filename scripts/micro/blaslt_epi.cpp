@@ -64,7 +64,9 @@ int main() {
                     {"proj", 32768, 768, 768, true}, {"fc1_bias_only", 32768, 3072, 768, false},
                     {"dec_256x512", 688128, 256, 512, false}, {"dec_256x256", 688128, 256, 256, false},
                     {"dec_128x256", 688128, 128, 256, false}, {"dec_384x256", 688128, 384, 256, false},
-                    {"fc1_gelu", 32768, 3072, 768, false, 1}};
+                    {"fc1_gelu", 32768, 3072, 768, false, 1},
+                    {"tok_256x256", 1176, 256, 256, false}, {"tok_2048x256", 1176, 2048, 256, false},
+                    {"tok_256x2048", 1176, 256, 2048, false}};
   const char* only = std::getenv("SHAPES");
   for (const Shape& s : shapes) {
     if (only) {  // SHAPES: comma list of name prefixes
@@ -131,7 +133,33 @@ int main() {
       if (s.f32_inplace) CK(hipMemcpyAsync(Dref, D0, nD * es, hipMemcpyDeviceToDevice, st));
       CK(octsam_gemm(&g, st));
     };
+    const bool graph_mode = std::getenv("GRAPH") != nullptr;
+    auto time_graph = [&](auto&& fn) {
+      hipGraph_t gr;
+      hipGraphExec_t ge;
+      CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      for (int i = 0; i < 50; ++i) fn();
+      CK(hipStreamEndCapture(st, &gr));
+      CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0));
+      CK(hipEventCreate(&e1));
+      float best = 1e30f;
+      for (int it = 0; it < 5; ++it) {
+        CK(hipEventRecord(e0, st));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::min(best, ms * 1e3f / 50);
+      }
+      hipGraphExecDestroy(ge);
+      hipGraphDestroy(gr);
+      return best;
+    };
     auto time_it = [&](auto&& fn, bool reset) {
+      if (graph_mode) return time_graph(fn);
       hipEvent_t e0, e1;
       CK(hipEventCreate(&e0));
       CK(hipEventCreate(&e1));
