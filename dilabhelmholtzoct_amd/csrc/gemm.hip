@@ -2520,9 +2520,10 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 
 // hipBLASLt for the plain in-place-residual encoder GEMMs (blaslt.cpp)
 bool blaslt_eligible(const octsam_gemm_args* a);
-int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s, bool f16);
+int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s);
 extern int g_blaslt_enabled;
 extern int g_blaslt_qkv;
+extern int g_blaslt_tok;
 
 // launch options and the last path taken are shared by the bf16 and fp16 builds of this file (the bf16
 // build owns them; the fp16 build reaches them through these hidden accessors), so
@@ -2551,6 +2552,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_res_lds = (enable & 4096) ? 0 : 1;
   g_blaslt_enabled = (enable & 65536) ? 0 : 1;
   g_blaslt_qkv = (enable & 131072) ? 0 : 1;
+  g_blaslt_tok = (enable & 262144) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2588,7 +2590,7 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   // (bf16 only: the fp16 encoder of configs[4] measured slower on hipBLASLt, 133.2 -> 129.2 imgs/s for vit-h,
   // profiles/r05/blaslt_vith_ab.log)
   if (g_use_glds == 1 && blaslt_eligible(a)) {
-    const int r = blaslt_gemm(a, (hipStream_t)stream, false);
+    const int r = blaslt_gemm(a, (hipStream_t)stream);
     if (r != 0) {
       t_last_path = 5;
       return r < 0 ? 1 : 0;

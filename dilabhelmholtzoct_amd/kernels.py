@@ -64,7 +64,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
         c_rows=_mapped_rows(out, ldc, residual, ldr, pre_out) if row_map is not None else 0,
         a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
-    if M >= 8192:  # (the sizes octsam_gemm may hand to hipBLASLt)
+    if M >= 1024:  # (the sizes octsam_gemm may hand to hipBLASLt)
         _gemm_workspace(out.device)
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out

@@ -42,9 +42,11 @@ def main():
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
                 "dkeys_joint": ({}, {"fuse_dkeys": True}), "dkeys_two": ({}, {"fuse_dkeys": False}),
                 "tokgroup_off": ({}, {"tok_group": False}), "g4w_off": ({}, {}),
-                "blaslt_off": ({}, {}), "blaslt_qkv_off": ({}, {})}
+                "blaslt_off": ({}, {}), "blaslt_qkv_off": ({}, {}),
+                "blaslt_tok_off": ({}, {})}
     FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512, "blaslt_off": 1 | 65536,
-            "blaslt_qkv_off": 1 | 131072}
+            "blaslt_qkv_off": 1 | 131072,
+            "blaslt_tok_off": 1 | 262144}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):

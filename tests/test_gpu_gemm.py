@@ -187,7 +187,7 @@ def test_gemm8_register_epilogue_act(cuda, act, M, N, K):
     bias = torch.randn(N, generator=g).to(cuda)
     R = torch.randn(M, N, generator=g).to(cuda, torch.bfloat16)
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    lib.octsam_gemm_set_fast_path(1 | 256)
+    lib.octsam_gemm_set_fast_path(1 | 256 | 262144)  # (262144: not hipBLASLt's token-side kind either)
     kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=bias, act=act, residual=R)
     assert lib.octsam_gemm_last_path() == 2
     lib.octsam_gemm_set_fast_path(1)
@@ -466,7 +466,7 @@ def test_gemm_blaslt_inplace_residual(cuda, M, N, K, bias):
     assert torch.equal(outs[0], outs[1])
     assert _rel(outs[0], outs[2]) < 1e-5
     x = X0[:4096].clone()
-    lib.octsam_gemm_set_fast_path(1 | 256)  # (256: not the small-problem kernel either)
+    lib.octsam_gemm_set_fast_path(1 | 256 | 262144)  # (256 / 262144: not the small kernel, not the token kind)
     kernels.gemm(A[:4096], W, M=4096, N=N, K=K, out=x, bias=b, residual=x)
     assert lib.octsam_gemm_last_path() == 2
     lib.octsam_gemm_set_fast_path(1)
@@ -501,6 +501,50 @@ def test_gemm_blaslt_qkv(cuda, M, N, K):
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
     kernels.gemm(A, W, M=M, N=N, K=K, out=out, bias=b, act=2)
     assert lib.octsam_gemm_last_path() == 2
+
+
+@pytest.mark.parametrize("b_mode", [0, 1])
+@pytest.mark.parametrize("kind", ["bias_f32", "relu_b16", "beta_acc", "residual"])
+@pytest.mark.parametrize("M,N,K", [(1176, 256, 256), (1176, 256, 2048), (1176, 2048, 256)])
+def test_gemm_blaslt_token_side(cuda, M, N, K, b_mode, kind):
+    """The decoder's token-side GEMMs (1024 <= M < 8192) on the hipBLASLt path (path 5): NT and k-major weights,
+    fp32 D + bias, bf16 D + bias + ReLU, beta = 1 accumulation into D, a separate fp32 residual; against torch
+    fp32, bit-identical run to run, and close to the native kernels (fast path bit 262144)."""
+    from dilabhelmholtzoct_amd import _lib, kernels
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N * 3 + K * 7 + b_mode + len(kind))
+    A = torch.randn(M, K, generator=g).to(cuda, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda, torch.bfloat16)
+    Bop = W if b_mode == 0 else W.t().contiguous()
+    b = torch.randn(N, generator=g).to(cuda)
+    D0 = torch.randn(M, N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda)
+    pre = A.float() @ W.float().t()
+    outs = []
+    for fast in (1, 1, 1 | 262144):
+        lib.octsam_gemm_set_fast_path(fast)
+        if kind == "bias_f32":
+            out = torch.empty(M, N, device=cuda)
+            kernels.gemm(A, Bop, M=M, N=N, K=K, out=out, b_mode=b_mode, bias=b)
+            ref, tol = pre + b, 1e-5
+        elif kind == "relu_b16":
+            out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+            kernels.gemm(A, Bop, M=M, N=N, K=K, out=out, b_mode=b_mode, bias=b, act=1)
+            ref, tol = F.relu(pre + b), 8e-3
+        elif kind == "beta_acc":
+            out = D0.clone()
+            kernels.gemm(A, Bop, M=M, N=N, K=K, out=out, b_mode=b_mode, beta=1.0)
+            ref, tol = pre + D0, 1e-5
+        else:
+            out = torch.empty(M, N, device=cuda)
+            kernels.gemm(A, Bop, M=M, N=N, K=K, out=out, b_mode=b_mode, bias=b, residual=R)
+            ref, tol = pre + b + R, 1e-5
+        assert lib.octsam_gemm_last_path() == (5 if fast == 1 else 3)
+        outs.append(out)
+    lib.octsam_gemm_set_fast_path(1)
+    assert _rel(outs[0], ref) < tol
+    assert torch.equal(outs[0], outs[1])
+    assert _rel(outs[0], outs[2]) < tol
 
 
 def test_gemm_small_path_ktotal(cuda):
