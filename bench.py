@@ -129,7 +129,7 @@ class GemmEventTimer:
                 out = orig(A, B, **kw)
                 e.record()
                 path = lib.octsam_gemm_last_path()
-                if path == 5:  # hipBLASLt (encoder MLP2 / projection): reported beside the family, not in it
+                if path == 5:  # hipBLASLt (csrc/blaslt.cpp): reported beside the family, not in it
                     self.lib_events.append((s, e, 2.0 * kw["M"] * kw["N"] * kw["K"]))
                 if path == 2:
                     fl = 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
@@ -163,14 +163,16 @@ class GemmEventTimer:
         return ms, n, self.flops
 
     def library(self):
-        """The GEMMs octsam_gemm hands to hipBLASLt (path 5: the encoder's in-place-residual MLP2 / projection)."""
+        """The GEMMs octsam_gemm hands to hipBLASLt (path 5: the encoder's QKV / projection / MLP2, the decoder's
+        token-side products)."""
         if not self.lib_events:
             return None
         ms = sum(s.elapsed_time(e) for s, e, _ in self.lib_events)
         fl = sum(f for _, _, f in self.lib_events)
         a = fl / (ms * 1e-3) / 1e12
-        return {"kernel": "hipBLASLt (octsam_gemm path 5: encoder MLP2 + attention projection, x += A W^T + b on "
-                          "the fp32 residual stream)", "bound": "mfma", "achieved": round(a, 2),
+        return {"kernel": "hipBLASLt (octsam_gemm path 5: the encoder's QKV, attention projection and MLP2 -- the "
+                          "last two x += A W^T + b on the fp32 residual stream -- and the decoder's token-side "
+                          "products)", "bound": "mfma", "achieved": round(a, 2),
                 "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(a / MI355X_BF16_DENSE_TFLOPS, 4),
                 "launches": len(self.lib_events), "avg_launch_us": round(ms * 1e3 / len(self.lib_events), 2)}
 
