@@ -95,8 +95,9 @@ def parse():
 
 def dominant_name(args) -> str:
     e = "bf16" if args.dtype == "bf16" else "fp16 (encoder) / bf16 (decoder)"
-    return (f"gemm8_kernel<0, EPI> family (8-phase 256x256 {e} NT GEMM, with its persistent form and the two-"
-            "workgroup 256x128 gemm4w_kernel: encoder QKV/proj/MLP, neck, decoder projections)")
+    return (f"gemm8w_kernel / gemm8_kernel family (256x256 {e} NT GEMMs: the ping-pong 8-wave kernel, the 8-phase "
+            "kernel and its persistent form, and the two-workgroup 256x128 gemm4w_kernel: the encoder's QKV, "
+            "attention projection, MLP1 and MLP2, the neck, the decoder's image-side projections)")
 
 
 class GemmEventTimer:
@@ -113,7 +114,6 @@ class GemmEventTimer:
         self.events = []
         self.flops = 0.0
         self.bytes = 0.0
-        self.lib_events = []
 
     def __enter__(self):
         orig = self.orig
@@ -129,8 +129,6 @@ class GemmEventTimer:
                 out = orig(A, B, **kw)
                 e.record()
                 path = lib.octsam_gemm_last_path()
-                if path == 5:  # hipBLASLt (csrc/blaslt.cpp): reported beside the family, not in it
-                    self.lib_events.append((s, e, 2.0 * kw["M"] * kw["N"] * kw["K"]))
                 if path == 2:
                     fl = 2.0 * kw["M"] * kw["N"] * kw["K"] * kw.get("batch", 1)
                     # compulsory bytes: A, B read once, C written once (+ residual read), per launch
@@ -161,20 +159,6 @@ class GemmEventTimer:
         ms = sum(s.elapsed_time(e) for s, e, _, _ in self.events)
         n = len(self.events)
         return ms, n, self.flops
-
-    def library(self):
-        """The GEMMs octsam_gemm hands to hipBLASLt (path 5: the encoder's QKV / projection / MLP2, the decoder's
-        token-side products)."""
-        if not self.lib_events:
-            return None
-        ms = sum(s.elapsed_time(e) for s, e, _ in self.lib_events)
-        fl = sum(f for _, _, f in self.lib_events)
-        a = fl / (ms * 1e-3) / 1e12
-        return {"kernel": "hipBLASLt (octsam_gemm path 5: the encoder's QKV, attention projection and MLP2 -- the "
-                          "last two x += A W^T + b on the fp32 residual stream -- and the decoder's token-side "
-                          "products)", "bound": "mfma", "achieved": round(a, 2),
-                "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s", "frac": round(a / MI355X_BF16_DENSE_TFLOPS, 4),
-                "launches": len(self.lib_events), "avg_launch_us": round(ms * 1e3 / len(self.lib_events), 2)}
 
     def by_bound(self):
         """The family's launches split by their compulsory arithmetic intensity against the MI355X ridge
@@ -620,7 +604,7 @@ def main():
     step = FusedTrainStep(model, lr=1e-3, topological=bool(args.top), process_group=pg, graphs=not args.eager,
                           pipeline=pipe)
     step.fork_topo = bool(args.fork_topo)
-    if args.gemm_fast_path != 1:  # (A/B of octsam_gemm's paths, e.g. 65537: no hipBLASLt)
+    if args.gemm_fast_path != 1:  # (A/B of octsam_gemm's paths, e.g. 8193: the 8-phase kernel instead of the ping-pong one)
         from dilabhelmholtzoct_amd import _lib
         _lib.load().octsam_gemm_set_fast_path(args.gemm_fast_path)
 
@@ -747,7 +731,6 @@ def main():
                     "launches": n, "avg_launch_us": round(ms * 1e3 / n, 2),
                     "share_of_step": round(ms / args.roof_steps / (dt * 1e3 / args.steps), 4)}
             roof["family_by_intensity"] = timer.by_bound()
-            roof["library_gemm"] = timer.library()
             roof.update(split)
 
     e2e = None

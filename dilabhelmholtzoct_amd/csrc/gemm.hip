@@ -1701,6 +1701,217 @@ int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Ping-pong 8-wave kernel (gemm8w): the same 256x256x64 tile, wave tiles (2 M x 4 N waves of 128 x 64), LDS
+// images and epilogues as gemm8, but each K-step of a wave is TWO segments between barriers instead of eight:
+//   L(t): the wave's 24 fragments of K-step t (8 A row blocks, 4 B column blocks, 2 k-halves; ds_read_b128 by
+//         inline asm into registers) plus its share of the LDS-DMA for later stages;
+//   C(t): all 64 of its 16x16x32 MFMAs of K-step t (1024 MFMA cycles, no LDS access).
+// The two wave rows run one segment apart (waves w and w+4 share a SIMD), so every segment pairs one wave's
+// matrix cluster with its SIMD partner's loads; gemm8's phases were 16 MFMAs (256 cycles) per barrier.
+// Stage t lives in buffer t & 1 ([A 256 x 64 | B 256 x 64] e16, 64 KiB); A rows 0-127 are read only by wave row
+// 0 (segment 2t), rows 128-255 only by wave row 1 (segment 2t+1), B by both, so each region is refilled as soon
+// as its last reader has passed a barrier, with the DMA split evenly over the loading waves:
+//   wave row 0 in L(t) (segment 2t):     B(t+1)                    -> landed at the end of its C(t): vmcnt(0)
+//   wave row 1 in L(t) (segment 2t+1):   A-hi(t+1), A-lo(t+2)      -> A-hi(t+1) landed at the end of its C(t)
+//                                                                     (vmcnt 4), A-lo(t+1) (issued in L(t-1))
+//                                                                     at the end of L(t) (vmcnt 8)
+//   prologue (all waves): stage 0 and A-lo(1).
+// Operands through buffer descriptors (rows past M / N read as zero); each 1 KiB DMA piece is 8 rows x 128 B, its
+// lane part of the offset depends only on the piece's parity (the chunk swizzle (r >> 1) & 7 of sw_off<64>).
+namespace pp8 {
+__device__ __forceinline__ void rd(e16x8& d, const char* base, int off) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(base + off)));
+}
+}  // namespace pp8
+
+// DBG 3 (diagnostics, fast path 9 with bit 8192): per workgroup s_memtime at entry, at the end of wave row 0's and
+// of wave row 1's main loop and after the epilogue's stores (octsam_gemm_debug_stamps)
+template <int EPI, int FE, int DBG = 0>
+__global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  long long st0 = 0;
+  if constexpr (DBG == 3) st0 = __builtin_amdgcn_s_memtime();
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = bid / per_batch, rem = bid - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 256;
+  const e16* A = (const e16*)p.A + bz * p.sA + (long long)row0 * p.lda;
+  const e16* B = (const e16*)p.B + bz * p.sB + (long long)col0 * p.ldb;
+  const int nk = p.K / 64;
+  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (p.M - row0) * lda2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (p.N - col0) * ldb2, 0x00020000);
+  uint32_t va[2], vb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    va[e] = (uint32_t)(r * lda2 + c * 16);
+    vb[e] = (uint32_t)(r * ldb2 + c * 16);
+  }
+  // piece j (8 rows) of A rows [h*128, h*128+128) / of B, K-step kt, into stage buffer buf
+  auto dma_a = [&](int h, int j, int kt) {
+    char* dst = gsm + (kt & 1) * ph8::BUF + (h * 128 + j * 8) * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)dst, 16, va[j & 1], (h * 128 + (j & ~1) * 8) * lda2 + kt * 128,
+                                             0, 0);
+  };
+  auto dma_b = [&](int j, int kt) {
+    char* dst = gsm + (kt & 1) * ph8::BUF + 32768 + j * 8 * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1], (j & ~1) * 8 * ldb2 + kt * 128, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+  e16x8 af[8][2], bf[4][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
+
+  // prologue: stage 0 (A-lo 2, A-hi 2, B 4 pieces per wave) and A-lo(1) (2 per wave)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(1, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_b(wave * 4 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 1);
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // wave row 1 runs one segment behind
+
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = gsm + (t & 1) * ph8::BUF;
+    // ---- L(t): DMA share, then the fragments of K-step t
+    if (wr == 0) {
+      if (t + 1 < nk) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma_b(wc * 8 + i, t + 1);
+      }
+    } else {
+      if (t + 1 < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(1, wc * 4 + i, t + 1);
+      }
+      if (t + 2 < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) pp8::rd(bf[ni][kb], cur + 32768, sw_off<64>(brow + ni * 16, kb * 4 + kq));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) pp8::rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wr == 1) {  // A-lo(t+1), issued in L(t-1), before wave row 0 reads it in the next segment
+      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    // ---- C(t): the wave's 64 MFMAs
+    if (t == 0) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], acc[mi][ni], 0, 0, 0);
+    }
+    if (wr == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(t+1)
+      raw_barrier();
+    } else {
+      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t+1)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t + 1 < nk) raw_barrier();
+    }
+  }
+  const int row0w = row0 + wr * 128, col0w = col0 + wc * 64;
+  if constexpr (DBG == 3) {
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if ((wave & 3) == 0 && lane == 0 && blockIdx.x < STAMP_WG) g_stamps[4 * blockIdx.x + 1 + wr] = t1;
+  }
+  bool done = false;
+  if constexpr (FE == 4) {
+    if (p.res_lds) {  // every stage buffer is free: each wave's two 8 KiB residual regions
+      char* bx = gsm + wave * 8192;
+      ph8::res_dma_q(p, bz, row0w, col0w, 0, bx, lane);
+      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0w, col0w, lane, bx, gsm + ph8::BUF + wave * 8192);
+      done = true;
+    }
+  }
+  if (!done) {
+    if constexpr (FE == 1) {
+      ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0w, col0w, lane);
+    } else {
+      ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0w, col0w, lane);
+      ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0w, col0w, lane);
+    }
+  }
+  if constexpr (DBG == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const long long t2 = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && blockIdx.x < STAMP_WG) {
+      g_stamps[4 * blockIdx.x] = st0;
+      g_stamps[4 * blockIdx.x + 3] = t2;
+    }
+  }
+}
+
+template <int EPI, int FE, int DBG = 0>
+int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + 255) / 256;
+  constexpr int LDS = 2 * ph8::BUF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8w_kernel<EPI, FE, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS);
+    attr = true;
+  }
+  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
+  hipLaunchKernelGGL((gemm8w_kernel<EPI, FE, DBG>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+// kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
+template <int EPI>
+int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool stamped = false) {
+  if (stamped) {  // (diagnostics)
+    if (k.fast_epi == 1) return launch_gemm8w_fe<EPI, 1, 3>(k, a, s);
+    if (k.fast_epi == 4) return launch_gemm8w_fe<EPI, 4, 3>(k, a, s);
+    return -1;
+  }
+  switch (k.fast_epi) {
+    case 1: return launch_gemm8w_fe<EPI, 1>(k, a, s);
+    case 2: return launch_gemm8w_fe<EPI, 2>(k, a, s);
+    case 4: return launch_gemm8w_fe<EPI, 4>(k, a, s);
+    case 8: return launch_gemm8w_fe<EPI, 8>(k, a, s);
+    default: return -1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // 256x192 variant of the 8-phase kernel for GEMMs whose 256-column tiles quantise badly on the chip (MLP2 /
 // proj at M = 32768, N = 768: 384 tiles = 1.5 waves of 256 CUs -> 512 tiles of 3/4 the work = 2 full waves).
 // Same phases, barriers and stagger; each wave owns 128 x 48 (3 column blocks of 16): Q(., 0) covers blocks
@@ -2160,6 +2371,8 @@ static int g_gemm4w = 1;
 static int g_gemm4w_res = 1;
 static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off: A/B)
 static int g_res_lds = 1;  // gemm8 fp32 residual kind through LDS (fast path bit 4096 turns it off: A/B)
+static int g_gemm8w = 1;   // ping-pong kernel (gemm8w) for the shapes gemm8 takes (fast path bit 8192 turns it off: A/B)
+static int g_gemm8w4 = 0;  // ... and for those gemm4w takes (fast path bit 16384 turns it on: A/B)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
@@ -2518,12 +2731,6 @@ __global__ __launch_bounds__(256) void splitk_reduce16_kernel(const float4* __re
 
 }  // namespace
 
-// hipBLASLt for the plain in-place-residual encoder GEMMs (blaslt.cpp)
-bool blaslt_eligible(const octsam_gemm_args* a);
-int blaslt_gemm(const octsam_gemm_args* a, hipStream_t s);
-extern int g_blaslt_enabled;
-extern int g_blaslt_qkv;
-extern int g_blaslt_tok;
 
 // launch options and the last path taken are shared by the bf16 and fp16 builds of this file (the bf16
 // build owns them; the fp16 build reaches them through these hidden accessors), so
@@ -2550,9 +2757,8 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_gemm4w_res = (enable & 1024) ? 0 : 1;
   g_rgroup = (enable & 2048) ? 0 : 1;
   g_res_lds = (enable & 4096) ? 0 : 1;
-  g_blaslt_enabled = (enable & 65536) ? 0 : 1;
-  g_blaslt_qkv = (enable & 131072) ? 0 : 1;
-  g_blaslt_tok = (enable & 262144) ? 0 : 1;
+  g_gemm8w = (enable & 8192) ? 0 : 1;
+  g_gemm8w4 = (enable & 16384) ? 1 : 0;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -2586,17 +2792,6 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
   if (a->a_mode == 3)
     OCTSAM_CHECK_ARG(a->conv_c % 8 == 0 && a->K == 9 * a->conv_c && a->M % 4096 == 0,
                      "octsam_gemm: conv3x3 mode needs K=9*C, C%%8==0, M=B*4096");
-#ifndef OCTSAM_GEMM_F16
-  // (bf16 only: the fp16 encoder of configs[4] measured slower on hipBLASLt, 133.2 -> 129.2 imgs/s for vit-h,
-  // profiles/r05/blaslt_vith_ab.log)
-  if (g_use_glds == 1 && blaslt_eligible(a)) {
-    const int r = blaslt_gemm(a, (hipStream_t)stream);
-    if (r != 0) {
-      t_last_path = 5;
-      return r < 0 ? 1 : 0;
-    }
-  }
-#endif
   GemmK k;
   k.A2 = a->A2; k.B2 = a->B2; k.a2_rows = a->a2_rows; k.b2_rows = a->b2_rows;
   k.a_blk = a->a_blk; k.a_rep = a->a_rep > 0 ? a->a_rep : 1;
@@ -2686,6 +2881,13 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       if (g_use_glds == 6) return launch_gemm8<1, 0>(k, a, s);
       if (g_use_glds == 7) return launch_gemm8<2, 0>(k, a, s);
       if (g_use_glds == 8) return launch_gemm8<0, -1>(k, a, s);
+      if (g_use_glds == 9 && g_gemm8w && am == 0 && bm == 0 && a->K % 64 == 0 && a->K >= 128 &&
+          (long long)a->M * a->lda * 2 < (1LL << 31) && (long long)a->N * a->ldb * 2 < (1LL << 31) &&
+          (a->act == 0 || a->act == OCTSAM_ACT_GELU)) {  // stamped ping-pong kernel (diagnostics)
+        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s, true)
+                                                : launch_gemm8w<0>(k, a, s, true);
+        if (r >= 0) return r;
+      }
       if (g_use_glds == 9) {  // stamped one-tile-per-workgroup kernel (diagnostics)
         if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<3, OCTSAM_ACT_GELU>(k, a, s);
         return launch_gemm8<3, 0>(k, a, s);
@@ -2698,6 +2900,15 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
       // (measured, scripts/gemm_ab.py, profiles/r03/gemm_ab.log: faster for N, K <= 1024 — proj 76 -> 69 us,
       // decoder ConvT1 178 -> 173 us — and slower for the wide / deep ones: QKV 129 -> 140, MLP1 179 -> 194, MLP2
       // 184 -> 195 us, where the 8-phase interleave of one 256x256 workgroup keeps the matrix pipes busier)
+      const bool w_ok = (g_use_glds == 1 || g_use_glds == 9) && am == 0 && bm == 0 && a->K % 64 == 0 && a->K >= 128 &&
+                        (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
+                        (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 31) &&
+                        (long long)a->N * a->ldb * 2 < (1LL << 31);
+      if (w_ok && g_gemm8w4) {
+        t_last_path = 2;
+        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);
+        if (r >= 0) return r;
+      }
       if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->K <= 1024 && a->N <= 1024 &&
           a->batch == 1 && am == 0 && bm == 0 &&
           a->M >= 4096 &&
@@ -2728,6 +2939,10 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
         if (a->act == OCTSAM_ACT_RELU) return launch_gemm8p<OCTSAM_ACT_RELU>(k, a, s, dbg);
         if (a->act == OCTSAM_ACT_GELU) return launch_gemm8p<OCTSAM_ACT_GELU>(k, a, s, dbg);
         return launch_gemm8p<0>(k, a, s, dbg);
+      }
+      if (w_ok && g_gemm8w) {
+        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);
+        if (r >= 0) return r;
       }
       if (a->act == OCTSAM_ACT_RELU) return launch_gemm8<0, OCTSAM_ACT_RELU>(k, a, s);
       if (a->act == OCTSAM_ACT_GELU) return launch_gemm8<0, OCTSAM_ACT_GELU>(k, a, s);

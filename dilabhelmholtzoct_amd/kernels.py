@@ -64,26 +64,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
         c_rows=_mapped_rows(out, ldc, residual, ldr, pre_out) if row_map is not None else 0,
         a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
-    if M >= 1024:  # (the sizes octsam_gemm may hand to hipBLASLt)
-        _gemm_workspace(out.device)
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
-
-
-GEMM_WORKSPACE_BYTES = 64 << 20
-_GEMM_WS = {}  # device index -> workspace tensor handed to octsam_gemm_set_workspace (kept alive here)
-
-
-def _gemm_workspace(dev: torch.device):
-    """The hipBLASLt path's workspace on dev (octsam_gemm_set_workspace), allocated on the first large GEMM of the
-    process (the eager pass before any graph capture; never from inside a capture)."""
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx in _GEMM_WS or torch.cuda.is_current_stream_capturing():
-        return
-    ws = torch.empty(GEMM_WORKSPACE_BYTES, dtype=torch.uint8, device=dev)
-    with torch.cuda.device(idx):
-        _lib.call("octsam_gemm_set_workspace", ptr(ws), GEMM_WORKSPACE_BYTES)
-    _GEMM_WS[idx] = ws
 
 
 def _span_rows(t: torch.Tensor, ld: int) -> int:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define OCTSAM_ABI_VERSION 23
+#define OCTSAM_ABI_VERSION 24
 
 #define OCTSAM_ACT_NONE 0
 #define OCTSAM_ACT_RELU 1
@@ -91,20 +91,12 @@ int octsam_gemm(const octsam_gemm_args* args, void* stream);
  * BASELINE configs[4] (sam-vit-huge, fp16) */
 int octsam_gemm_f16(const octsam_gemm_args* args, void* stream);
 /* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing);
-   bit 256 disables the small-problem tile kernel, bit 512 the two-workgroups-per-CU 256x128 kernel, bit 65536 the
-   hipBLASLt path, bit 131072 its QKV kind, bit 262144 its token-side kind */
+   bit 256 disables the small-problem tile kernel, bit 512 the two-workgroups-per-CU 256x128 kernel. Every path is a
+   hand-written kernel of this library (ABI 24: the hipBLASLt path of ABI 23 and its octsam_gemm_set_workspace are
+   gone). */
 void octsam_gemm_set_fast_path(int32_t enable);
-/* Workspace (device memory owned by the caller, current device) for octsam_gemm's hipBLASLt path: the plain
-   in-place-residual GEMM x += A W^T (+ bias) with x fp32 (R == C), bf16 K-contiguous operands (octsam_gemm; the
-   fp16 octsam_gemm_f16 stays native), one batch, no activation, M >= 8192, N >= 256, K >= 512 -- the ViT encoder's
-   MLP2 and attention projection -- and a bf16 D = A W^T + bias without residual, M >= 8192, 2048 <= N <= 4096,
-   K <= 1024 -- the QKV projection -- and at 1024 <= M < 8192 the mask decoder's token-side products (NT or k-major
-   weights, fp32 or bf16 D, bias, ReLU, beta * D, or a separate same-type residual) (replaces the same
-   octsam_gemm call; hf:modeling_sam.py SamVisionLayer.forward residual adds). Without a workspace (or bytes = 0)
-   those GEMMs run on the native kernels. ABI 23. */
-int octsam_gemm_set_workspace(void* workspace, int64_t bytes);
 /* which kernel the calling thread's last octsam_gemm launched: 0 generic tile kernel, 1 persistent
-   global_load_lds kernel, 2 8-phase / two-workgroup kernels, 3 small-problem kernel, 5 hipBLASLt. Used to
+   global_load_lds kernel, 2 8-phase / ping-pong / two-workgroup kernels, 3 small-problem kernel. Used to
    attribute per-kernel timings. */
 int32_t octsam_gemm_last_path(void);
 /* diagnostics: fast path 9 runs the one-tile-per-workgroup 8-phase kernel with per-workgroup s_memtime stamps

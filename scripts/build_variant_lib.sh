@@ -10,5 +10,5 @@ mkdir -p build/ab $R/ab_libs
 EXTRA=""
 [ $F = vit_attention.hip ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1 -fno-honor-nans -mno-amdgpu-ieee"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $EXTRA $FLAGS -c $F -o build/ab/variant.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/ab_libs/$NAME.so build/ab/variant.o $(ls build/*.o | grep -v "build/${F}.o") -lhipblaslt
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/ab_libs/$NAME.so build/ab/variant.o $(ls build/*.o | grep -v "build/${F}.o")
 ls -la $R/ab_libs/$NAME.so

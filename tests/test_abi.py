@@ -39,7 +39,7 @@ def test_abi_version_and_error_channel():
     import re
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                             "octsam.h")).read()
-    assert lib.octsam_abi_version() == int(re.search(r"#define OCTSAM_ABI_VERSION (\d+)", hdr).group(1)) == 23
+    assert lib.octsam_abi_version() == int(re.search(r"#define OCTSAM_ABI_VERSION (\d+)", hdr).group(1)) == 24
     assert isinstance(lib.octsam_last_error(), (bytes, type(None)))
 
 

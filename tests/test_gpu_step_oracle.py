@@ -1,7 +1,9 @@
-"""One training step of BASELINE configs[1] - configs[4]'s per-GPU slices on the HIP path against the oracle
+"""One training step of BASELINE configs[0]'s workload and configs[1] - configs[4]'s per-GPU slices on the HIP path against the oracle
 (oracle/step_ref.py: transformers SamModel fp32 + restated DiceCE / topo loss, run on the GPU here only for
 speed) on the same synthetic weights and batch:
 
+* configs[0]: sam-vit-base, box prompts, --top=False, one image (the reference's CPU plumbing case) through the
+  HIP path;
 * configs[1]: sam-vit-base, box prompts, --top=False, bf16, 8 images per GPU (the DiceCE-only step,
   ref:octsam/models/training_utils.py:62-68 with topological=False);
 * configs[2]: the same with --top=True (the bench's workload);
@@ -19,6 +21,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 CASES = {  # name: (model, prompt, images, encoder dtype, topological)
+    # configs[0]'s workload (the reference's own CPU-runnable case: vit-b, boxes, --top=False, one image) on the GPU
+    "vitb_bboxes_b1_top_off": ("facebook/sam-vit-base", "bboxes", 1, torch.bfloat16, False),
     "vitb_bboxes_b8_top_off": ("facebook/sam-vit-base", "bboxes", 8, torch.bfloat16, False),
     "vitb_bboxes_b8_top_on": ("facebook/sam-vit-base", "bboxes", 8, torch.bfloat16, True),
     "vitl_points_b4_bf16": ("facebook/sam-vit-large", "points", 4, torch.bfloat16, True),

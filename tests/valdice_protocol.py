@@ -61,6 +61,97 @@ def host_batches(seed: int, n: int, epoch: int):
             for s in range(0, n, BS)]
 
 
+class _CachedImages:
+    """The PIL SamImageProcessor behind a cache keyed by the images' bytes: a batch's images are the same in every
+    epoch (only its prompts are redrawn), so the oracle's host path resizes each batch once. Returns a new
+    BatchFeature over the cached tensors (SamProcessor adds the prompts to it)."""
+
+    def __init__(self, real):
+        self.real = real
+        self.cache = {}
+
+    def __getattr__(self, name):
+        return getattr(self.real, name)
+
+    def __call__(self, images, **kw):
+        import hashlib
+
+        import numpy as np
+        from transformers import BatchFeature
+        arr = np.asarray(images.numpy() if hasattr(images, "numpy") else images)
+        key = (hashlib.sha1(arr.tobytes()).hexdigest(), arr.shape, tuple(sorted((k, str(v)) for k, v in kw.items())))
+        if key not in self.cache:
+            self.cache[key] = self.real(images, **kw)
+        enc = self.cache[key]
+        return BatchFeature(dict(enc), tensor_type=None)
+
+
+_FAST = {}
+
+
+def fast_host_batches(seed: int, n: int, epoch: int):
+    """host_batches, bit-identical (tests/test_valdice_fast_host.py), for the oracle's many seed pairs: the same
+    SAMDataset prompt draws (seed_sample, then per component in scipy / np.unique order the bbox jitter
+    np.random.randint(-10, 10) x 4, training_utils.py:402-411) and the same SamProcessor call for the boxes, but
+    each scan's connected components are labelled once per seed (not once per epoch), the gt masks are built as
+    uint8 directly (the reference's float64 masks are exactly 0 / 1, process_batch rounds them to uint8), and the
+    images' resize / normalisation is cached across epochs (_CachedImages)."""
+    import numpy as np
+    from torch.nn.utils.rnn import pad_sequence
+
+    from dilabhelmholtzoct_amd import data
+    if "proc" not in _FAST:
+        proc = data.make_processor()
+        proc.image_processor = _CachedImages(proc.image_processor)
+        _FAST["proc"] = proc
+    proc = _FAST["proc"]
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+
+    def label_one(d):
+        lab = np.array(d["label"])
+        comps = []
+        for v, labeled, c in data.SAMDataset._components(lab):
+            m = labeled == c + 1
+            y_idx, x_idx = np.where(m)
+            comps.append((v, m, int(np.min(x_idx)), int(np.max(x_idx)), int(np.min(y_idx)), int(np.max(y_idx))))
+        return np.array(d["image"]), comps, lab.shape
+
+    if (seed, n) not in _FAST:
+        with ThreadPoolExecutor(workers) as ex:
+            _FAST[seed, n] = list(ex.map(label_one, data.synthetic_oct(seed=seed, n=n)))
+    items = _FAST[seed, n]
+    calls = []
+    for s in range(0, n, BS):
+        idx = range(s, min(n, s + BS))
+        imgs, boxes, gts, vals = [], [], [], []
+        for i in idx:
+            data.seed_sample(epoch, i, seed)
+            img, comps, (H, W) = items[i]
+            bb = []
+            for v, m, x0, x1, y0, y1 in comps:
+                x0 = max(0, x0 + np.random.randint(-10, 10))
+                x1 = min(W, x1 + np.random.randint(-10, 10))
+                y0 = max(0, y0 + np.random.randint(-10, 10))
+                y1 = min(H, y1 + np.random.randint(-10, 10))
+                bb.append([x0, y0, x1, y1])
+            imgs.append(img)
+            boxes.append(torch.tensor(bb))
+            gts.append(torch.from_numpy(np.stack([m for _, m, *_ in comps]).astype(np.uint8)))
+            vals.append(torch.tensor([v for v, *_ in comps]))
+        calls.append((torch.tensor(np.array(imgs)), pad_sequence(boxes, batch_first=True),
+                      pad_sequence(gts, batch_first=True), pad_sequence(vals, batch_first=True)))
+
+    def process(c):
+        inputs = dict(proc(c[0], input_boxes=c[1], return_tensors="pt"))
+        inputs["gt_u8"] = c[2]
+        inputs["mask_values"] = c[3]
+        return inputs
+
+    with ThreadPoolExecutor(workers) as ex:  # (PIL and numpy release the GIL in the resize / normalisation)
+        return list(ex.map(process, calls))
+
+
 @contextlib.contextmanager
 def oracle_mode():
     """The oracle's torch ops, run-to-run reproducible: MIOpen off (its solution choice for the decoder's
@@ -246,7 +337,7 @@ class OracleRunner:
     def conf(self, ref, val_seed):
         from oracle.eval_ref import pooled_confusion_ref
         if val_seed not in self._val:
-            self._val[val_seed] = host_batches(val_seed, N_VAL, 0)
+            self._val[val_seed] = fast_host_batches(val_seed, N_VAL, 0)
         c = torch.zeros(14, 4, dtype=torch.int64)
         with torch.no_grad(), oracle_mode():
             for i, v in enumerate(self._val[val_seed]):
@@ -256,7 +347,7 @@ class OracleRunner:
 
     def train_steps(self, ref, seed, epoch, limit=None):
         """One epoch (or its first `limit` steps) of oracle steps on the training seed; -> steps taken."""
-        tr = host_batches(seed, N_TRAIN, epoch)
+        tr = fast_host_batches(seed, N_TRAIN, epoch)
         k = 0
         for i, b in enumerate(tr):
             if limit is not None and k >= limit:
