@@ -109,6 +109,9 @@ struct GemmK {
   float* b_cs;
   int rgroup;    // broadcast-residual tile order (rgroup_tm); 0 = plain order
   int res_lds;   // gemm8 in-place fp32 residual kind: residual through LDS (ph8::epilogue_res_lds)
+  float* sk_part;  // gemm8s (stream-K): partial slots [grid][256 x 256] fp32 and their flags [grid] (caller's workspace)
+  int* sk_flag;
+  int sk_batch;
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -1722,10 +1725,180 @@ namespace pp8 {
 __device__ __forceinline__ void rd(e16x8& d, const char* base, int off) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(base + off)));
 }
+
+// The ping-pong main loop over K-steps [kb0, kb0 + n) of one 256x256 tile (n >= 1): acc = sum over those K-steps
+// (the first K-step's MFMAs start from zero). Stage t of the loop lives in buffer t & 1. Every wave enters and leaves
+// with the same barrier count (wave row 1 takes one extra at the start and skips the last); on return wave row 0 is
+// one segment ahead (its epilogue overlaps wave row 1's last MFMA cluster) and every LDS read of the loop is done.
+// SKIP (diagnostics, wrong results): bit 1 no DMA after the prologue, bit 2 no fragment reads, bit 4 no MFMAs;
+// bit 8: the DMA pieces are issued in the wave's MFMA segment (one after every 4 MFMAs) instead of its load segment
+template <bool ZACC = true, int SKIP = 0>  // ZACC: the first K-step's MFMAs start from zero (else from acc: zeroed)
+__device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int kb0, int n,
+                                         f32x4 (&acc)[8][4], char* gsm, int wave, int lane) {
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + (long long)row0 * p.lda), (short)0, (p.M - row0) * lda2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B + (long long)col0 * p.ldb), (short)0, (p.N - col0) * ldb2, 0x00020000);
+  uint32_t va[2], vb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    va[e] = (uint32_t)(r * lda2 + c * 16);
+    vb[e] = (uint32_t)(r * ldb2 + c * 16);
+  }
+  // piece j (8 rows) of A rows [h*128, h*128+128) / of B, loop stage t (K-step kb0 + t) into buffer t & 1
+  auto dma_a = [&](int h, int j, int t) {
+    char* dst = gsm + (t & 1) * ph8::BUF + (h * 128 + j * 8) * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)dst, 16, va[j & 1],
+                                             (h * 128 + (j & ~1) * 8) * lda2 + (kb0 + t) * 128, 0, 0);
+  };
+  auto dma_b = [&](int j, int t) {
+    char* dst = gsm + (t & 1) * ph8::BUF + 32768 + j * 8 * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1], (j & ~1) * 8 * ldb2 + (kb0 + t) * 128,
+                                             0, 0);
+  };
+  e16x8 af[8][2], bf[4][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
+
+  // prologue: stage 0 (A-lo 2, A-hi 2, B 4 pieces per wave) and A-lo(1) (2 per wave)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(1, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_b(wave * 4 + i, 0);
+  if (n > 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // wave row 1 runs one segment behind
+
+  for (int t = 0; t < n; ++t) {
+    const char* cur = gsm + (t & 1) * ph8::BUF;
+    // ---- L(t): DMA share, then the fragments of K-step t
+    constexpr bool DMA_IN_C = (SKIP & 8) != 0;
+    if ((SKIP & 1) || DMA_IN_C) {
+    } else if (wr == 0) {
+      if (t + 1 < n) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma_b(wc * 8 + i, t + 1);
+      }
+    } else {
+      if (t + 1 < n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(1, wc * 4 + i, t + 1);
+      }
+      if (t + 2 < n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2 && !(SKIP & 2); ++kb) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) rd(bf[ni][kb], cur + 32768, sw_off<64>(brow + ni * 16, kb * 4 + kq));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wr == 1 && DMA_IN_C) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A-lo(t+1), issued in C(t-1)
+    } else if (wr == 1) {  // A-lo(t+1), issued in L(t-1), before wave row 0 reads it in the next segment
+      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (t + 1 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    // ---- C(t): the wave's 64 MFMAs
+    if constexpr ((SKIP & 4) != 0) {
+      if (t == 0)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = __builtin_bit_cast(f32x4, af[mi][0]) + __builtin_bit_cast(f32x4, bf[ni][1]);
+    } else if (!DMA_IN_C && ZACC && t == 0) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
+    } else if (DMA_IN_C) {
+      // the wave's DMA share, one piece after every 4 MFMAs (sched_group_barrier: 4 MFMA, 1 VMEM)
+      const bool z = ZACC && t == 0;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], (z && kb == 0) ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
+          const int q = kb * 8 + mi;
+          if (q < 8) {
+            if (wr == 0) {
+              if (t + 1 < n) dma_b(wc * 8 + q, t + 1);
+            } else if (q < 4) {
+              if (t + 1 < n) dma_a(1, wc * 4 + q, t + 1);
+            } else {
+              if (t + 2 < n) dma_a(0, wc * 4 + q - 4, t + 2);
+            }
+          }
+        }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], acc[mi][ni], 0, 0, 0);
+    }
+    if (wr == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(t+1)
+      raw_barrier();
+    } else {
+      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t+1)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t + 1 < n) raw_barrier();
+    }
+  }
+}
+
+// the tile's epilogue (the lean kinds of epilogue_fast; the in-place fp32 residual through LDS, ph8::epilogue_res_lds,
+// in the LDS the main loop no longer reads)
+template <int EPI, int FE>
+__device__ __forceinline__ void epilogue(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0w, int col0w, char* gsm,
+                                         int wave, int lane) {
+  if constexpr (FE == 4) {
+    if (p.res_lds) {
+      char* bx = gsm + wave * 8192;
+      ph8::res_dma_q(p, bz, row0w, col0w, 0, bx, lane);
+      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0w, col0w, lane, bx, gsm + ph8::BUF + wave * 8192);
+      return;
+    }
+  }
+  if constexpr (FE == 1) {
+    ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0w, col0w, lane);
+  } else {
+    ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0w, col0w, lane);
+    ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0w, col0w, lane);
+  }
+}
 }  // namespace pp8
 
-// DBG 3 (diagnostics, fast path 9 with bit 8192): per workgroup s_memtime at entry, at the end of wave row 0's and
-// of wave row 1's main loop and after the epilogue's stores (octsam_gemm_debug_stamps)
+// DBG 3 (diagnostics, fast path 9): per workgroup s_memtime at entry, at the end of wave row 0's and of wave row 1's
+// main loop and after the epilogue's stores (octsam_gemm_debug_stamps)
 template <int EPI, int FE, int DBG = 0>
 __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
@@ -1742,129 +1915,14 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
   const int bz = bid / per_batch, rem = bid - bz * per_batch;
   const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
   const int row0 = tm * 256, col0 = tn * 256;
-  const e16* A = (const e16*)p.A + bz * p.sA + (long long)row0 * p.lda;
-  const e16* B = (const e16*)p.B + bz * p.sB + (long long)col0 * p.ldb;
-  const int nk = p.K / 64;
-  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (p.M - row0) * lda2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (p.N - col0) * ldb2, 0x00020000);
-  uint32_t va[2], vb[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-    va[e] = (uint32_t)(r * lda2 + c * 16);
-    vb[e] = (uint32_t)(r * ldb2 + c * 16);
-  }
-  // piece j (8 rows) of A rows [h*128, h*128+128) / of B, K-step kt, into stage buffer buf
-  auto dma_a = [&](int h, int j, int kt) {
-    char* dst = gsm + (kt & 1) * ph8::BUF + (h * 128 + j * 8) * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)dst, 16, va[j & 1], (h * 128 + (j & ~1) * 8) * lda2 + kt * 128,
-                                             0, 0);
-  };
-  auto dma_b = [&](int j, int kt) {
-    char* dst = gsm + (kt & 1) * ph8::BUF + 32768 + j * 8 * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1], (j & ~1) * 8 * ldb2 + kt * 128, 0, 0);
-  };
-
   f32x4 acc[8][4];
-  e16x8 af[8][2], bf[4][2];
-  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
-
-  // prologue: stage 0 (A-lo 2, A-hi 2, B 4 pieces per wave) and A-lo(1) (2 per wave)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 0);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) dma_a(1, wave * 2 + i, 0);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dma_b(wave * 4 + i, 0);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 1);
-  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  raw_barrier();
-  if (wr == 1) raw_barrier();  // wave row 1 runs one segment behind
-
-  for (int t = 0; t < nk; ++t) {
-    const char* cur = gsm + (t & 1) * ph8::BUF;
-    // ---- L(t): DMA share, then the fragments of K-step t
-    if (wr == 0) {
-      if (t + 1 < nk) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dma_b(wc * 8 + i, t + 1);
-      }
-    } else {
-      if (t + 1 < nk) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dma_a(1, wc * 4 + i, t + 1);
-      }
-      if (t + 2 < nk) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
-      }
-    }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) pp8::rd(bf[ni][kb], cur + 32768, sw_off<64>(brow + ni * 16, kb * 4 + kq));
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) pp8::rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (wr == 1) {  // A-lo(t+1), issued in L(t-1), before wave row 0 reads it in the next segment
-      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    raw_barrier();
-    // ---- C(t): the wave's 64 MFMAs
-    if (t == 0) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], acc[mi][ni], 0, 0, 0);
-    }
-    if (wr == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(t+1)
-      raw_barrier();
-    } else {
-      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t+1)
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (t + 1 < nk) raw_barrier();
-    }
-  }
-  const int row0w = row0 + wr * 128, col0w = col0 + wc * 64;
+  pp8::mainloop<true, (DBG >= 16 ? DBG - 16 : 0)>(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, 0,
+                                                   p.K / 64, acc, gsm, wave, lane);
   if constexpr (DBG == 3) {
     const long long t1 = __builtin_amdgcn_s_memtime();
     if ((wave & 3) == 0 && lane == 0 && blockIdx.x < STAMP_WG) g_stamps[4 * blockIdx.x + 1 + wr] = t1;
   }
-  bool done = false;
-  if constexpr (FE == 4) {
-    if (p.res_lds) {  // every stage buffer is free: each wave's two 8 KiB residual regions
-      char* bx = gsm + wave * 8192;
-      ph8::res_dma_q(p, bz, row0w, col0w, 0, bx, lane);
-      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0w, col0w, lane, bx, gsm + ph8::BUF + wave * 8192);
-      done = true;
-    }
-  }
-  if (!done) {
-    if constexpr (FE == 1) {
-      ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0w, col0w, lane);
-    } else {
-      ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0w, col0w, lane);
-      ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0w, col0w, lane);
-    }
-  }
+  pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
   if constexpr (DBG == 3) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1873,6 +1931,96 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
       g_stamps[4 * blockIdx.x] = st0;
       g_stamps[4 * blockIdx.x + 3] = t2;
     }
+  }
+}
+
+// Stream-K form of the ping-pong kernel (gemm8s): one workgroup per CU (grid G), the flat sequence of T tiles x nk
+// K-steps cut into G equal ranges (each >= nk, so a tile has at most two parts). A workgroup runs its range as
+// pieces: first the tail of the tile its range starts in (K-steps k0..nk: its fp32 accumulators go to partial slot g
+// of the workspace by write-through (sc1) stores, then every wave's vmcnt(0), a barrier and an sc1 flag store), then
+// its whole tiles (ordinary epilogue), then the head of the tile its range ends in (K-steps 0..k1: after the main
+// loop one lane polls slot g+1's flag with sc1 loads, a barrier, the partial comes in by sc1 loads and is added --
+// head + tail, one fp32 add, so the result is the same whichever part finishes first -- the flag is reset for the
+// next launch and the ordinary epilogue runs). The hand-off is MI355X_MICROARCH's first valid row (sc1 stores,
+// drained, one flag per storing workgroup, sc1 loads). Partial slots are stored in the accumulator layout (each
+// lane's 32 f32x4 as consecutive 1 KiB wave rows), so both sides read / write whole lines. Deadlock-free without
+// co-residency: a producer's tail is the first piece of its range and waits for nothing.
+template <int EPI, int FE>
+__global__ __launch_bounds__(512, 2) void gemm8s_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm_[];
+  const int tid = threadIdx.x, lane_ = tid & 63, wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave_ >> 2, wc = wave_ & 3;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int nk = p.K / 64, per_batch = p.tiles_m * p.tiles_n;
+  const long long total = (long long)per_batch * p.sk_batch * nk;
+  const long long lo = total * g / G, hi = total * (g + 1) / G;
+  float* slot_base = p.sk_part;  // [G][8 waves][32][64 lanes] f32x4
+  const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(slot_base), (short)0, 0x7fffffff, 0x00020000);
+  f32x4 acc[8][4];
+  long long it = lo;
+  bool first = true;
+  while (it < hi) {
+    const int tile = (int)(it / nk), k0 = (int)(it - (long long)tile * nk);
+    const int k1 = (int)min((long long)nk, hi - (long long)tile * nk);
+    const int bz = tile / per_batch, rem = tile - bz * per_batch;
+    const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+    const int row0 = tm * 256, col0 = tn * 256;
+    if (!first) raw_barrier();  // the previous piece's epilogue is done with the LDS
+    first = false;
+    // (an opaque zero: the main loop's and epilogue's address arithmetic is redone per piece instead of hoisted out of
+    //  this loop, where it would stay live across every piece and spill)
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const int wave = wave_ + z, lane = lane_ + z;
+    char* gsm = gsm_ + z;
+    const uint32_t lane_off = (uint32_t)((wave * 32 * 64 + lane) * 16);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4)0.0f;
+    pp8::mainloop<false>(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, k0, k1 - k0, acc, gsm,
+                         wave, lane);
+    if (k0 > 0) {  // tail of a tile: publish the partial for the head's owner (workgroup g - 1)
+      const uint32_t sbase = (uint32_t)g * (8u * 32u * 64u * 16u);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rpart,
+                                                 lane_off + (uint32_t)((mi * 4 + ni) * 1024), sbase, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (tid == 0) __hip_atomic_store(p.sk_flag + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (k1 < nk) {  // head of a tile: add the tail's partial (slot g + 1)
+        if (tid == 0) {
+          while (__hip_atomic_load(p.sk_flag + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            __builtin_amdgcn_s_sleep(2);
+        }
+        raw_barrier();
+        const uint32_t sbase = (uint32_t)(g + 1) * (8u * 32u * 64u * 16u);
+#pragma unroll
+        for (int m2 = 0; m2 < 8; m2 += 2) {  // two row blocks at a time (32 VGPRs in flight beside the accumulators)
+          f32x4 v[2][4];
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              v[mi][ni] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rpart, lane_off + (uint32_t)(((m2 + mi) * 4 + ni) * 1024), sbase, 16 /* sc1 */));
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) acc[m2 + mi][ni] = acc[m2 + mi][ni] + v[mi][ni];
+          asm volatile("" ::: "memory");
+        }
+        if (tid == 0) __hip_atomic_store(p.sk_flag + g + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
+    }
+    it = (long long)tile * nk + k1;
   }
 }
 
@@ -1894,9 +2042,70 @@ int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
   return 0;
 }
 
+template <int EPI, int FE>
+int launch_gemm8s_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, int G) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = (a->N + 255) / 256;
+  g.sk_batch = a->batch;
+  g.sk_part = (float*)a->workspace;
+  g.sk_flag = (int*)((char*)a->workspace + (size_t)G * 262144);
+  constexpr int LDS = 2 * ph8::BUF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm8s_kernel<EPI, FE>), dim3((unsigned)G), dim3(512), LDS, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
+
+static int sk_grid() {  // one workgroup per CU
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+  }
+  return n_cu;
+}
+
+// stream-K when the tiles fill the chip's waves badly (fewer than 0.9 of the last wave's workgroups busy on average,
+// e.g. the encoder's MLP2: 384 tiles = 1.5 waves) and every range holds at least one whole tile; -1: not taken
+template <int EPI>
+int launch_gemm8s(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
+  const int G = sk_grid();
+  const long long T = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
+  const long long waves = (T + G - 1) / G;
+  if (T < G || (double)T / (double)(waves * G) >= 0.9 || a->workspace == nullptr ||
+      a->workspace_bytes < (long long)G * (262144 + 4) || ((uintptr_t)a->workspace & 255) != 0)
+    return -1;
+  switch (k.fast_epi) {
+    case 1: return launch_gemm8s_fe<EPI, 1>(k, a, s, G);
+    case 2: return launch_gemm8s_fe<EPI, 2>(k, a, s, G);
+    case 4: return launch_gemm8s_fe<EPI, 4>(k, a, s, G);
+    default: return -1;
+  }
+}
+
 // kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
 template <int EPI>
 int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool stamped = false) {
+  if (g_pp_skip) {  // (diagnostics: the main loop without DMA / fragment reads / MFMAs; wrong results)
+    if (k.fast_epi != 1) return -1;
+    switch (g_pp_skip) {
+      case 1: return launch_gemm8w_fe<EPI, 1, 17>(k, a, s);
+      case 2: return launch_gemm8w_fe<EPI, 1, 18>(k, a, s);
+      case 4: return launch_gemm8w_fe<EPI, 1, 20>(k, a, s);
+      case 3: return launch_gemm8w_fe<EPI, 1, 19>(k, a, s);
+      case 5: return launch_gemm8w_fe<EPI, 1, 24>(k, a, s);  // (fast path bits: 5 << 20 = DMA in the MFMA segment)
+      default: return -1;
+    }
+  }
   if (stamped) {  // (diagnostics)
     if (k.fast_epi == 1) return launch_gemm8w_fe<EPI, 1, 3>(k, a, s);
     if (k.fast_epi == 4) return launch_gemm8w_fe<EPI, 4, 3>(k, a, s);
@@ -2373,6 +2582,7 @@ static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off
 static int g_res_lds = 1;  // gemm8 fp32 residual kind through LDS (fast path bit 4096 turns it off: A/B)
 static int g_gemm8w = 1;   // ping-pong kernel (gemm8w) for the shapes gemm8 takes (fast path bit 8192 turns it off: A/B)
 static int g_gemm8w4 = 0;  // ... and for those gemm4w takes (fast path bit 16384 turns it on: A/B)
+static int g_gemm8s = 0;   // its stream-K form where the tiles quantise badly (fast path bit 32768 turns it on: A/B)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
@@ -2759,10 +2969,13 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_res_lds = (enable & 4096) ? 0 : 1;
   g_gemm8w = (enable & 8192) ? 0 : 1;
   g_gemm8w4 = (enable & 16384) ? 1 : 0;
+  g_gemm8s = (enable & 32768) ? 1 : 0;
+  g_pp_skip = (enable >> 20) & 7;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
+extern "C" int64_t octsam_gemm_workspace_bytes(void) { return (int64_t)sk_grid() * (262144 + 4); }
 extern "C" int octsam_gemm_debug_stamps(int64_t* host, int32_t n_wg) {
   OCTSAM_CHECK_ARG(host && n_wg > 0 && n_wg <= STAMP_WG, "octsam_gemm_debug_stamps: bad args");
   const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n_wg * 4 * sizeof(long long));
@@ -2904,6 +3117,11 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
                         (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
                         (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 31) &&
                         (long long)a->N * a->ldb * 2 < (1LL << 31);
+      if (w_ok && g_gemm8s && (g_gemm8w4 || !(a->K <= 1024 && a->N <= 1024))) {
+        t_last_path = 2;
+        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8s<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8s<0>(k, a, s);
+        if (r >= 0) return r;
+      }
       if (w_ok && g_gemm8w4) {
         t_last_path = 2;
         const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);

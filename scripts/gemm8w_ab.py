@@ -12,7 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dilabhelmholtzoct_amd import _lib, kernels as K  # noqa: E402
 
 lib = _lib.load()
-VARIANTS = {"native": 1 | 8192, "w": 1, "w4": 1 | 16384}
+VARIANTS = {"native": 1 | 8192, "w": 1, "w4": 1 | 16384, "sk": 1 | 32768,
+            # diagnostics of the ping-pong loop (wrong results except dmac): no DMA / no fragment reads / no MFMAs
+            "skipdma": 1 | (1 << 20), "skiprd": 1 | (2 << 20), "skipmfma": 1 | (4 << 20), "skipdmard": 1 | (3 << 20),
+            "dmac": 1 | (5 << 20)}
 if os.environ.get("VARIANTS"):
     VARIANTS = {k: VARIANTS[k] for k in os.environ["VARIANTS"].split(",")}
 
@@ -32,7 +35,7 @@ def t(fn, it=20):
 
 # (name, M, N, K, act, residual)
 SHAPES = [("qkv", 32768, 2304, 768, 0, 0), ("proj", 32768, 768, 768, 0, 1), ("fc1", 32768, 3072, 768, 2, 0),
-          ("fc2", 32768, 768, 3072, 0, 1), ("neck1", 32768, 256, 768, 0, 0), ("dec_up1", 688128, 256, 256, 0, 0),
+          ("fc2", 32768, 768, 3072, 0, 1), ("fc2e16", 32768, 768, 3072, 0, 0), ("neck1", 32768, 256, 768, 0, 0), ("dec_up1", 688128, 256, 256, 0, 0),
           ("ragged", 5000, 1000, 320, 0, 0), ("ragged_res", 3000, 520, 192, 0, 1)]
 if os.environ.get("SHAPES"):
     SHAPES = [s for s in SHAPES if s[0] in os.environ["SHAPES"].split(",")]

@@ -15,7 +15,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 echo "pmc fetch ok"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc/write -o run -- python3 $R/bench.py $SHORT > $O/pmc_write.log 2>&1 || exit 1
 echo "pmc write ok"
-python3 $R/scripts/pmc_traffic.py $O/pmc gemm8_kernel,gemm8p_kernel,gemm4w_kernel $O/traffic_gemm_family.json || exit 1
+python3 $R/scripts/pmc_traffic.py $O/pmc gemm8w_kernel,gemm8_kernel,gemm8p_kernel,gemm4w_kernel $O/traffic_gemm_family.json || exit 1
 cp $O/traffic_gemm_family.json $R/profiles/traffic_gemm_family.json
 python3 $R/scripts/pmc_kernels.py $O/pmc $O/traffic_kernels.json > $O/traffic_kernels.txt || exit 1
 rm -rf $O/pmc
