@@ -444,25 +444,28 @@ def val_protocol(args, device):
     t0 = time.perf_counter()
     epoch_batches = P.device_batches(device)
     state, adam = P.load_warm()
+    runner = P.HipRunner(device, state, epoch_batches)
     pairs = []
     for tr, va in P.SEEDS:
-        hip = [round(P.dice_of(c), 5) for _, c in P.hip_run(device, state, adam, tr, va, epoch_batches=epoch_batches,
-                                                               val_batches=epoch_batches(va, P.N_VAL, 0))]
+        hip = [round(P.dice_of(c), 5) for _, c in runner.run(state, adam, tr, va,
+                                                              val_batches=epoch_batches(va, P.N_VAL, 0))]
         g = gold_pairs[(tr, va)]
         pairs.append({"train_seed": tr, "val_seed": va, "hip": hip, "oracle": g["oracle_dice"],
                       "diff": [round(h - o, 5) for h, o in zip(hip, g["oracle_dice"])],
-                      "oracle_spread": g["spread"]})
+                      "oracle_perturbed": P.perturbed_of(g), "oracle_spread": g.get("spread")})
+    del runner
     n = len(pairs)
     mean_diff = [round(sum(p["diff"][i] for p in pairs) / n, 5) for i in range(len(P.CHECKPOINTS))]
     verdict = P.mean_diff_verdict([p["hip"] for p in pairs], [p["oracle"] for p in pairs],
-                                  [p["oracle_spread"] for p in pairs])
-    out = {"steps": P.CHECKPOINTS, "pairs": pairs, "mean_diff": mean_diff,
+                                  [p["oracle_perturbed"] for p in pairs])
+    out = {"steps": P.CHECKPOINTS, "n_pairs": n, "mean_diff": mean_diff,
+           "se": [v["se"] for v in verdict], "noise_floor_mean": [v.get("noise_floor_mean") for v in verdict],
            "max_abs_mean_diff": round(max(abs(d) for d in mean_diff), 5), "tolerance": P.TOL,
            "within": bool(max(abs(d) for d in mean_diff) <= P.TOL), "checkpoints": verdict,
-           "within_resolution": all(v["ok"] for v in verdict), "seconds": round(time.perf_counter() - t0, 1),
+           "seconds": round(time.perf_counter() - t0, 1),
            "protocol": "tests/valdice_protocol.py (oracle-made warm start; per seed pair 4 epochs x 16 steps; 32 "
-                       "held-out scans; mean over pairs of Dice_HIP - Dice_oracle)",
-           "oracle_source": "tests/golden/valdice_oracle.json"}
+                       "held-out scans; strict |mean over pairs of Dice_HIP - Dice_oracle| <= tolerance)",
+           "oracle_source": "tests/golden/valdice_oracle.json", "pairs": pairs}
     log(f"val protocol: mean diff {mean_diff} ({out['seconds']} s)")
     torch.cuda.empty_cache()
     return out

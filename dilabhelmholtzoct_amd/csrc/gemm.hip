@@ -109,9 +109,9 @@ struct GemmK {
   float* b_cs;
   int rgroup;    // broadcast-residual tile order (rgroup_tm); 0 = plain order
   int res_lds;   // gemm8 in-place fp32 residual kind: residual through LDS (ph8::epilogue_res_lds)
-  float* sk_part;  // gemm8s (stream-K): partial slots [grid][256 x 256] fp32 and their flags [grid] (caller's workspace)
-  int* sk_flag;
-  int sk_batch;
+  float* sk_part;  // gemm8h (split-K by two): partial slots [tiles][256 x 256] fp32 (caller's workspace)
+  int* sk_flag;    // ... then the tiles' tickets [tiles] and flags [tiles]
+  int sk_batch;    // the number of tiles
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -385,6 +385,107 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmK p) {
       }
     }
   }
+}
+
+// Small problems with K <= 256 (the decoder's token-side products: M = prompts x 7 rows, N, K = 128-256): the
+// 64x64-tile kernel above chains one global load latency per 64-deep K-step (load, LDS store, barrier, MFMAs).
+// Here every K-step's operand chunks are loaded into registers at once (at most 4 stages x 2 operands x 2 chunks
+// of 16 B per thread), stored into a 4-stage LDS image, one barrier, then all MFMAs: one load latency per tile.
+// Same LDS image, fragments, MFMA order (the K-steps in sequence) and epilogue as gemm_kernel<AM, BMODE, 64>, so the
+// results are bit-identical to it.
+template <int AM, int BMODE>
+__global__ __launch_bounds__(NTHR, 2) void gemm_small_kernel(GemmK p) {
+  constexpr int T = 64, NS = 4;
+  __shared__ __attribute__((aligned(16))) e16 smem[NS * (T + T) * BK];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, loc = bid >> 3;
+    int q = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int row0 = tm * T, col0 = tn * T;
+  const int bz = blockIdx.y;
+  const void* Abase = (const void*)((const char*)p.A + bz * p.sA * 2);
+  const void* Bbase = (const void*)((const char*)p.B + bz * p.sB * 2);
+  const int kcap = p.k_total > 0 ? min(p.K, p.k_total - bz * p.K) : p.K;
+  const int nk = (p.K + BK - 1) / BK;  // <= NS (host-checked)
+  Loader<AM, T> la[NS];
+  Loader<BMODE, T> lb[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s < nk) {
+      la[s].load(p, Abase, p.A2, p.a2_rows, p.lda, p.M, row0, s * BK, tid, p.a_blk, p.a_rep, kcap);
+      lb[s].load(p, Bbase, p.B2, p.b2_rows, p.ldb, p.N, col0, s * BK, tid, p.b_blk, p.b_rep, kcap);
+    }
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s < nk) {
+      la[s].store(smem + s * (T + T) * BK, tid);
+      lb[s].store(smem + s * (T + T) * BK + T * BK, tid);
+    }
+  __syncthreads();
+  f32x16 acc = (f32x16)0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s >= nk) break;
+    const e16* sa = smem + s * (T + T) * BK;
+    const e16* sb = sa + T * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ch = kk * 2 + (lane >> 5);
+      const e16x8 af = *(const e16x8*)(sa + lds_idx(wm * (T / 2) + (lane & 31), ch));
+      const e16x8 bfr = *(const e16x8*)(sb + lds_idx(wn * (T / 2) + (lane & 31), ch));
+      acc = mma32(af, bfr, acc, 0, 0, 0);
+    }
+  }
+  char* Cb = (char*)p.C + bz * p.sC * (p.c_f32 ? 4 : 2);
+  const char* Rb = p.R ? (const char*)p.R + bz * p.sR * (p.r_f32 ? 4 : 2) : nullptr;
+  char* Pb = p.Cpre ? (char*)p.Cpre + bz * p.sC * (p.pre_f32 ? 4 : 2) : nullptr;
+  const int n = col0 + wn * (T / 2) + (lane & 31);
+  if (n >= p.N) return;
+  const float bv = p.bias ? p.bias[n] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = row0 + wm * (T / 2) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (m >= p.M) continue;
+    int om = m;
+    if (p.row_map) {
+      om = p.row_map[m];
+      if (om < 0) continue;
+    }
+    const long long ci = (long long)om * p.ldc + n;
+    float v = acc[r] * p.alpha;
+    if (p.beta != 0.0f) v += p.beta * (p.c_f32 ? ((float*)Cb)[ci] : (float)((e16*)Cb)[ci]);
+    v += bv;
+    if (Pb) {
+      if (p.pre_f32) ((float*)Pb)[ci] = v;
+      else ((e16*)Pb)[ci] = (e16)v;
+    }
+    if (p.act == OCTSAM_ACT_RELU) v = fmaxf(v, 0.0f);
+    else if (p.act == OCTSAM_ACT_GELU) v = gelu_erf(v);
+    if (Rb) {
+      const long long ri = remap(om, p.r_blk, p.r_rep) * p.ldr + n;
+      v += p.r_f32 ? ((const float*)Rb)[ri] : (float)((const e16*)Rb)[ri];
+    }
+    if (p.c_f32) ((float*)Cb)[ci] = v;
+    else ((e16*)Cb)[ci] = (e16)v;
+  }
+}
+
+template <int AM, int BMODE>
+int launch_small(const GemmK& k0, int batch, hipStream_t s) {
+  GemmK k = k0;
+  k.tiles_m = (k.M + 63) / 64;
+  k.tiles_n = (k.N + 63) / 64;
+  dim3 grid(k.tiles_m * k.tiles_n, batch);
+  hipLaunchKernelGGL((gemm_small_kernel<AM, BMODE>), grid, dim3(NTHR), 0, s, k);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
 }
 
 template <int AM, int BMODE, int T = 128>
@@ -1934,94 +2035,86 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
   }
 }
 
-// Stream-K form of the ping-pong kernel (gemm8s): one workgroup per CU (grid G), the flat sequence of T tiles x nk
-// K-steps cut into G equal ranges (each >= nk, so a tile has at most two parts). A workgroup runs its range as
-// pieces: first the tail of the tile its range starts in (K-steps k0..nk: its fp32 accumulators go to partial slot g
-// of the workspace by write-through (sc1) stores, then every wave's vmcnt(0), a barrier and an sc1 flag store), then
-// its whole tiles (ordinary epilogue), then the head of the tile its range ends in (K-steps 0..k1: after the main
-// loop one lane polls slot g+1's flag with sc1 loads, a barrier, the partial comes in by sc1 loads and is added --
-// head + tail, one fp32 add, so the result is the same whichever part finishes first -- the flag is reset for the
-// next launch and the ordinary epilogue runs). The hand-off is MI355X_MICROARCH's first valid row (sc1 stores,
-// drained, one flag per storing workgroup, sc1 loads). Partial slots are stored in the accumulator layout (each
-// lane's 32 f32x4 as consecutive 1 KiB wave rows), so both sides read / write whole lines. Deadlock-free without
-// co-residency: a producer's tail is the first piece of its range and waits for nothing.
+// Split-K-by-two form of the ping-pong kernel (gemm8h) for deep GEMMs whose 256x256 tiles fill the chip's waves
+// badly (the encoder's MLP2: K = 3072, 384 tiles = 1.5 waves of 256 CUs -> 768 half-tiles = 3 full waves). Workgroup
+// pair (2t, 2t + 1) (consecutive after the XCD remap, so they run in the same dispatch wave) computes tile t over K-steps
+// [0, nk/2) and [nk/2, nk). After its main loop a workgroup takes a ticket for the tile (agent-scope atomic add): the
+// first stores its fp32 accumulators to the tile's partial slot by write-through (sc1) stores, drains them (every
+// wave's vmcnt(0), a barrier) and sets the tile's flag (sc1 store); the second polls that flag (sc1 loads; the first
+// is resident and waits for nothing), reads the partial by sc1 loads, adds it (one fp32 add per element: the same bits
+// whichever half finishes first), resets ticket and flag for the next launch and runs the epilogue. The hand-off is
+// MI355X_MICROARCH's first valid row (sc1 stores, drained, one flag per storing workgroup, sc1 loads). Partial slots
+// hold the accumulator layout (each lane's 32 f32x4 as consecutive 1 KiB wave rows). Deterministic, not bit-identical
+// to the unsplit kernels (two partial sums instead of one chain).
 template <int EPI, int FE>
-__global__ __launch_bounds__(512, 2) void gemm8s_kernel(GemmK p) {
-  extern __shared__ __attribute__((aligned(16))) char gsm_[];
-  const int tid = threadIdx.x, lane_ = tid & 63, wave_ = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave_ >> 2, wc = wave_ & 3;
-  const int G = gridDim.x, g = blockIdx.x;
-  const int nk = p.K / 64, per_batch = p.tiles_m * p.tiles_n;
-  const long long total = (long long)per_batch * p.sk_batch * nk;
-  const long long lo = total * g / G, hi = total * (g + 1) / G;
-  float* slot_base = p.sk_part;  // [G][8 waves][32][64 lanes] f32x4
-  const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(slot_base), (short)0, 0x7fffffff, 0x00020000);
+__global__ __launch_bounds__(512, 2) void gemm8h_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  __shared__ int s_ticket;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int tile = bid >> 1, half = bid & 1;
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = tile / per_batch, rem = tile - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 256;
+  const int nk = p.K / 64, kh = nk >> 1;
   f32x4 acc[8][4];
-  long long it = lo;
-  bool first = true;
-  while (it < hi) {
-    const int tile = (int)(it / nk), k0 = (int)(it - (long long)tile * nk);
-    const int k1 = (int)min((long long)nk, hi - (long long)tile * nk);
-    const int bz = tile / per_batch, rem = tile - bz * per_batch;
-    const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
-    const int row0 = tm * 256, col0 = tn * 256;
-    if (!first) raw_barrier();  // the previous piece's epilogue is done with the LDS
-    first = false;
-    // (an opaque zero: the main loop's and epilogue's address arithmetic is redone per piece instead of hoisted out of
-    //  this loop, where it would stay live across every piece and spill)
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    const int wave = wave_ + z, lane = lane_ + z;
-    char* gsm = gsm_ + z;
-    const uint32_t lane_off = (uint32_t)((wave * 32 * 64 + lane) * 16);
+  pp8::mainloop(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, half ? kh : 0,
+                half ? nk - kh : kh, acc, gsm, wave, lane);
+  raw_barrier();  // (wave row 0 finished one segment earlier)
+  // (an opaque zero: nothing of the hand-off is computed before the main loop, where it would stay live and spill)
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  int* ticket = p.sk_flag + tile + z;
+  int* flag = p.sk_flag + p.sk_batch + tile + z;  // (sk_batch: the number of tiles, the tickets' length)
+  const __amdgpu_buffer_rsrc_t rpart =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.sk_part + z), (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t lane_off = (uint32_t)((wave * 32 * 64 + lane + z) * 16);
+  const uint32_t sbase = (uint32_t)(tile + z) * (8u * 32u * 64u * 16u);
+  if (tid == 0) s_ticket = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket == 0) {  // first half done: publish the partial
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4)0.0f;
-    pp8::mainloop<false>(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, k0, k1 - k0, acc, gsm,
-                         wave, lane);
-    if (k0 > 0) {  // tail of a tile: publish the partial for the head's owner (workgroup g - 1)
-      const uint32_t sbase = (uint32_t)g * (8u * 32u * 64u * 16u);
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rpart,
-                                                 lane_off + (uint32_t)((mi * 4 + ni) * 1024), sbase, 16 /* sc1 */);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      raw_barrier();
-      if (tid == 0) __hip_atomic_store(p.sk_flag + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (k1 < nk) {  // head of a tile: add the tail's partial (slot g + 1)
-        if (tid == 0) {
-          while (__hip_atomic_load(p.sk_flag + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            __builtin_amdgcn_s_sleep(2);
-        }
-        raw_barrier();
-        const uint32_t sbase = (uint32_t)(g + 1) * (8u * 32u * 64u * 16u);
-#pragma unroll
-        for (int m2 = 0; m2 < 8; m2 += 2) {  // two row blocks at a time (32 VGPRs in flight beside the accumulators)
-          f32x4 v[2][4];
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-              v[mi][ni] = __builtin_bit_cast(
-                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                             rpart, lane_off + (uint32_t)(((m2 + mi) * 4 + ni) * 1024), sbase, 16 /* sc1 */));
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) acc[m2 + mi][ni] = acc[m2 + mi][ni] + v[mi][ni];
-          asm volatile("" ::: "memory");
-        }
-        if (tid == 0) __hip_atomic_store(p.sk_flag + g + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
-    }
-    it = (long long)tile * nk + k1;
+      for (int ni = 0; ni < 4; ++ni)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rpart,
+                                               lane_off + (uint32_t)((mi * 4 + ni) * 1024), sbase, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (tid == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
+  if (tid == 0) {
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+  }
+  raw_barrier();
+#pragma unroll
+  for (int m2 = 0; m2 < 8; m2 += 2) {  // two row blocks at a time (32 VGPRs in flight beside the accumulators)
+    f32x4 v[2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        v[mi][ni] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rpart, lane_off + (uint32_t)(((m2 + mi) * 4 + ni) * 1024),
+                                                         sbase, 16 /* sc1 */));
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[m2 + mi][ni] = acc[m2 + mi][ni] + v[mi][ni];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (tid == 0) {
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
 }
 
 template <int EPI, int FE, int DBG = 0>
@@ -2043,27 +2136,28 @@ int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
 }
 
 template <int EPI, int FE>
-int launch_gemm8s_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, int G) {
+int launch_gemm8h_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, long long T) {
   GemmK g = k0;
   g.tiles_m = (a->M + 255) / 256;
   g.tiles_n = (a->N + 255) / 256;
-  g.sk_batch = a->batch;
+  g.sk_batch = (int)T;
   g.sk_part = (float*)a->workspace;
-  g.sk_flag = (int*)((char*)a->workspace + (size_t)G * 262144);
+  g.sk_flag = (int*)((char*)a->workspace + (size_t)T * 262144);
   constexpr int LDS = 2 * ph8::BUF;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8s_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    (void)hipFuncSetAttribute((const void*)gemm8h_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm8s_kernel<EPI, FE>), dim3((unsigned)G), dim3(512), LDS, s, g);
+  hipLaunchKernelGGL((gemm8h_kernel<EPI, FE>), dim3((unsigned)(2 * T)), dim3(512), LDS, s, g);
   OCTSAM_LAUNCH_CHECK("octsam_gemm");
   return 0;
 }
 
+static int g_small_oneshot = 1;  // K <= 256 small problems on gemm_small_kernel (fast path bit 65536 turns it off)
 static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
 
-static int sk_grid() {  // one workgroup per CU
+static int sk_grid() {  // CUs of the current device
   static int n_cu = 0;
   if (!n_cu) {
     int dev = 0;
@@ -2073,21 +2167,22 @@ static int sk_grid() {  // one workgroup per CU
   }
   return n_cu;
 }
+constexpr long long WS_BYTES = 192LL << 20;  // octsam_gemm_workspace_bytes: up to 768 split tiles
 
-// stream-K when the tiles fill the chip's waves badly (fewer than 0.9 of the last wave's workgroups busy on average,
-// e.g. the encoder's MLP2: 384 tiles = 1.5 waves) and every range holds at least one whole tile; -1: not taken
+// the split-K-by-two form where it fills the waves better: deep K (>= 1536: the partial round trip is small beside
+// a half tile's main loop) and half-tile waves 10 % shorter than whole-tile waves; -1: not taken
 template <int EPI>
-int launch_gemm8s(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
+int launch_gemm8h(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   const int G = sk_grid();
   const long long T = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
-  const long long waves = (T + G - 1) / G;
-  if (T < G || (double)T / (double)(waves * G) >= 0.9 || a->workspace == nullptr ||
-      a->workspace_bytes < (long long)G * (262144 + 4) || ((uintptr_t)a->workspace & 255) != 0)
+  const long long w1 = (T + G - 1) / G, w2 = (2 * T + G - 1) / G;
+  if (a->K < 1536 || (a->K / 64) < 4 || !(0.55 * (double)w2 < (double)w1) || a->workspace == nullptr ||
+      a->workspace_bytes < T * (262144 + 8) || ((uintptr_t)a->workspace & 255) != 0 || T > (1LL << 20))
     return -1;
   switch (k.fast_epi) {
-    case 1: return launch_gemm8s_fe<EPI, 1>(k, a, s, G);
-    case 2: return launch_gemm8s_fe<EPI, 2>(k, a, s, G);
-    case 4: return launch_gemm8s_fe<EPI, 4>(k, a, s, G);
+    case 1: return launch_gemm8h_fe<EPI, 1>(k, a, s, T);
+    case 2: return launch_gemm8h_fe<EPI, 2>(k, a, s, T);
+    case 4: return launch_gemm8h_fe<EPI, 4>(k, a, s, T);
     default: return -1;
   }
 }
@@ -2582,7 +2677,7 @@ static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off
 static int g_res_lds = 1;  // gemm8 fp32 residual kind through LDS (fast path bit 4096 turns it off: A/B)
 static int g_gemm8w = 1;   // ping-pong kernel (gemm8w) for the shapes gemm8 takes (fast path bit 8192 turns it off: A/B)
 static int g_gemm8w4 = 0;  // ... and for those gemm4w takes (fast path bit 16384 turns it on: A/B)
-static int g_gemm8s = 0;   // its stream-K form where the tiles quantise badly (fast path bit 32768 turns it on: A/B)
+static int g_gemm8s = 1;   // its split-K-by-two form where the tiles quantise badly (fast path bit 32768 turns it off)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
@@ -2969,13 +3064,14 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_res_lds = (enable & 4096) ? 0 : 1;
   g_gemm8w = (enable & 8192) ? 0 : 1;
   g_gemm8w4 = (enable & 16384) ? 1 : 0;
-  g_gemm8s = (enable & 32768) ? 1 : 0;
+  g_gemm8s = (enable & 32768) ? 0 : 1;
   g_pp_skip = (enable >> 20) & 7;
+  g_small_oneshot = (enable & 65536) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
-extern "C" int64_t octsam_gemm_workspace_bytes(void) { return (int64_t)sk_grid() * (262144 + 4); }
+extern "C" int64_t octsam_gemm_workspace_bytes(void) { return WS_BYTES; }
 extern "C" int octsam_gemm_debug_stamps(int64_t* host, int32_t n_wg) {
   OCTSAM_CHECK_ARG(host && n_wg > 0 && n_wg <= STAMP_WG, "octsam_gemm_debug_stamps: bad args");
   const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n_wg * 4 * sizeof(long long));
@@ -3061,6 +3157,12 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
     const long long t256 = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
     if (am <= 1 && bm <= 1 && a->a_blk == 0 && a->b_blk == 0 && t256 < 96 && t64 <= 4096 && g_small && !want_cs) {
       t_last_path = 3;
+      if (a->K <= 256 && g_small_oneshot) {
+        if (am == 0 && bm == 0) return launch_small<0, 0>(k, a->batch, s);
+        if (am == 0 && bm == 1) return launch_small<0, 1>(k, a->batch, s);
+        if (am == 1 && bm == 0) return launch_small<1, 0>(k, a->batch, s);
+        return launch_small<1, 1>(k, a->batch, s);
+      }
       if (am == 0 && bm == 0) return launch<0, 0, 64>(k, a->batch, s);
       if (am == 0 && bm == 1) return launch<0, 1, 64>(k, a->batch, s);
       if (am == 1 && bm == 0) return launch<1, 0, 64>(k, a->batch, s);
@@ -3119,7 +3221,7 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
                         (long long)a->N * a->ldb * 2 < (1LL << 31);
       if (w_ok && g_gemm8s && (g_gemm8w4 || !(a->K <= 1024 && a->N <= 1024))) {
         t_last_path = 2;
-        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8s<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8s<0>(k, a, s);
+        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8h<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8h<0>(k, a, s);
         if (r >= 0) return r;
       }
       if (w_ok && g_gemm8w4) {

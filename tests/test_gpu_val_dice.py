@@ -11,18 +11,18 @@ oracle values depend on no HIP kernel. For every seed pair of valdice_protocol.S
 * oracle: oracle/step_ref.py (transformers SamModel fp32 on the GPU, restated DiceCE / topo loss, torch Adam) in
   oracle_mode (bit-reproducible), scored by oracle/eval_ref.pooled_confusion_ref (training_utils.py:126-156): the
   committed values of tests/golden/valdice_oracle.json, and on the first LIVE_PAIRS pairs rerun live here.
-Asserted (valdice_protocol.mean_diff_verdict):
-* at every checkpoint where the oracle reproduces itself (its perturbation spread below the tolerance on every pair
-  that has one: steps 0-32), |mean over seed pairs of (Dice_HIP - Dice_oracle)| <= 0.005;
-* at the chaotic checkpoints (steps 48-64: the oracle's own Dice moves by up to 0.024 under bf16-sized weight
-  perturbations, and every variant of the HIP step tried -- bf16 or fp16 encoder, either keys-gradient form -- differs
-  from it by up to 0.03-0.05 on single pairs, missing or making the oracle's one-epoch dips), the mean difference is
-  not significantly outside the tolerance: |mean| <= 0.005 + 2 standard errors of the per-pair differences;
+Asserted (valdice_protocol.mean_diff_verdict), strictly:
+* at EVERY checkpoint (steps 0, 16, 32, 48, 64), |mean over the N_PAIRS = 96 seed pairs of (Dice_HIP - Dice_oracle)|
+  <= 0.005. Past step 32 single trajectories are chaotic (the oracle's own Dice moves by up to 0.024 under
+  bf16-sized weight perturbations; per-pair differences reach 0.03-0.05 either way), which is why the comparison is a
+  mean over 96 independent pairs: its 2 standard errors (~0.003) stay inside the tolerance, and there is no
+  allowance for noise in the bound. The oracle's own perturbed-minus-base mean (one bf16-sized perturbation of the
+  start state per pair, from the golden) is printed beside it as the noise floor;
 * the oracle is in the non-degenerate regime (mean specificity > 0.5), its Dice is a real segmentation (> 0.5) and the
   compared epochs trained (the oracle's decoder moved by more than 1 % in norm, its Dice changed);
 * the live oracle equals the committed golden (which bench.py quotes beside its own HIP run) within 1e-4 (same box
   type and software; oracle_mode makes it reproducible).
-Per pair the Dice difference and the oracle's own perturbation spread (from the golden) are printed."""
+Per pair the Dice difference and the oracle's perturbation spread (from the golden) are printed."""
 import json
 import os
 import sys
@@ -48,24 +48,24 @@ def test_val_dice_parity_multiseed(cuda):
     assert not missing, f"golden lacks pairs {missing}: make_valdice_golden.py --oracle --keep"
     runner = P.OracleRunner(cuda)
     epoch_batches = P.device_batches(cuda)
+    hip_runner = P.HipRunner(cuda, state, epoch_batches)
     rows = []
     for idx, (tr, va) in enumerate(P.SEEDS):
         g = gold_pairs[(tr, va)]
-        hip = [(k, P.dice_of(c)) for k, c in P.hip_run(cuda, state, adam, tr, va, epoch_batches=epoch_batches,
-                                                        val_batches=epoch_batches(va, P.N_VAL, 0))]
+        hip = [(k, P.dice_of(c)) for k, c in hip_runner.run(state, adam, tr, va,
+                                                             val_batches=epoch_batches(va, P.N_VAL, 0))]
         live = None
         if idx < P.LIVE_PAIRS:  # the oracle itself on this box, against its committed values
             ora_c, moved = runner.run(state, adam, tr, va)
             live = [P.dice_of(c) for _, c in ora_c]
             spec = mean_specificity_ref(ora_c[-1][1])
+            runner.forget(tr, va)
         else:
             moved, spec = g["oracle_moved"], g["oracle_specificity"]
         rows.append({"pair": (tr, va), "hip": [d for _, d in hip], "oracle": g["oracle_dice"], "live": live,
-                     "spec": spec, "moved": moved, "spread": g["spread"]})
-        for (k, h), o in zip(hip, g["oracle_dice"]):
-            print(f"pair {tr}/{va} after {k:3d} steps: val Dice HIP {h:.5f}  oracle {o:.5f}  diff {h - o:+.5f}")
-        print(f"pair {tr}/{va}: oracle specificity {spec:.4f}, decoder moved {moved:.4f}, live oracle {live}, "
-              f"oracle spread {g['spread']}")
+                     "spec": spec, "moved": moved, "spread": g.get("spread"), "perturbed": P.perturbed_of(g)})
+        print(f"pair {tr}/{va}: HIP {[round(d, 5) for _, d in hip]} oracle {g['oracle_dice']} diff "
+              f"{[round(h - o, 5) for (_, h), o in zip(hip, g['oracle_dice'])]} spread {g.get('spread')}")
     n = len(rows)
     mean_diff = [sum(r["hip"][i] - r["oracle"][i] for r in rows) / n for i in range(len(P.CHECKPOINTS))]
     print("mean over pairs of Dice_HIP - Dice_oracle per checkpoint:", [f"{d:+.5f}" for d in mean_diff])
@@ -82,7 +82,8 @@ def test_val_dice_parity_multiseed(cuda):
         if r["live"] is not None:
             dg = max(abs(a - b) for a, b in zip(r["live"], r["oracle"]))
             assert dg <= 1e-4, f"pair {r['pair']}: live oracle {r['live']} vs committed golden {r['oracle']}"
-    verdict = P.mean_diff_verdict([r["hip"] for r in rows], [r["oracle"] for r in rows], [r["spread"] for r in rows])
+    verdict = P.mean_diff_verdict([r["hip"] for r in rows], [r["oracle"] for r in rows],
+                                  [r["perturbed"] for r in rows])
     for v in verdict:
         print(json.dumps(v))
     bad = [v for v in verdict if not v["ok"]]
