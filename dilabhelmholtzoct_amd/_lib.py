@@ -36,7 +36,7 @@ class GemmArgs(ctypes.Structure):
         ("a2_rows", c_int32), ("b2_rows", c_int32),
         ("a_blk", c_int32), ("a_rep", c_int32), ("b_blk", c_int32), ("b_rep", c_int32),
         ("r_blk", c_int32), ("r_rep", c_int32), ("k_total", c_int32), ("c_rows", c_int32),
-        ("a_colsum", c_void_p), ("b_colsum", c_void_p), ("workspace", c_void_p), ("workspace_bytes", c_int64),
+        ("a_colsum", c_void_p), ("b_colsum", c_void_p),
     ]
 
 
@@ -48,7 +48,6 @@ _SIGNATURES = {
     "octsam_gemm_f16": (c_int32, [ctypes.POINTER(GemmArgs), c_void_p]),
     "octsam_gemm_set_fast_path": (None, [c_int32]),
     "octsam_gemm_last_path": (c_int32, []),
-    "octsam_gemm_workspace_bytes": (c_int64, []),
     "octsam_gemm_debug_stamps": (c_int32, [c_void_p, c_int32]),
     "octsam_splitk_reduce": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_float, c_void_p]),
     "octsam_wgrad_supported": (c_int32, [c_int64, c_int32, c_int32]),

@@ -109,9 +109,6 @@ struct GemmK {
   float* b_cs;
   int rgroup;    // broadcast-residual tile order (rgroup_tm); 0 = plain order
   int res_lds;   // gemm8 in-place fp32 residual kind: residual through LDS (ph8::epilogue_res_lds)
-  float* sk_part;  // gemm8h (split-K by two): partial slots [tiles][256 x 256] fp32 (caller's workspace)
-  int* sk_flag;    // ... then the tiles' tickets [tiles] and flags [tiles]
-  int sk_batch;    // the number of tiles
 };
 
 // repeat_interleave row remap: logical row -> stored row = (row / (blk*rep)) * blk + row % blk
@@ -1842,7 +1839,7 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
       (void*)(A + (long long)row0 * p.lda), (short)0, (p.M - row0) * lda2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(B + (long long)col0 * p.ldb), (short)0, (p.N - col0) * ldb2, 0x00020000);
-  uint32_t va[2], vb[2];
+  uint32_t va[2], vb[2];  // lane part of a DMA piece's offset (by the piece's parity: the chunk swizzle of sw_off<64>)
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
@@ -1857,8 +1854,8 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
   };
   auto dma_b = [&](int j, int t) {
     char* dst = gsm + (t & 1) * ph8::BUF + 32768 + j * 8 * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1], (j & ~1) * 8 * ldb2 + (kb0 + t) * 128,
-                                             0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1],
+                                             (j & ~1) * 8 * ldb2 + (kb0 + t) * 128, 0, 0);
   };
   e16x8 af[8][2], bf[4][2];
   const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
@@ -2035,88 +2032,6 @@ __global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
   }
 }
 
-// Split-K-by-two form of the ping-pong kernel (gemm8h) for deep GEMMs whose 256x256 tiles fill the chip's waves
-// badly (the encoder's MLP2: K = 3072, 384 tiles = 1.5 waves of 256 CUs -> 768 half-tiles = 3 full waves). Workgroup
-// pair (2t, 2t + 1) (consecutive after the XCD remap, so they run in the same dispatch wave) computes tile t over K-steps
-// [0, nk/2) and [nk/2, nk). After its main loop a workgroup takes a ticket for the tile (agent-scope atomic add): the
-// first stores its fp32 accumulators to the tile's partial slot by write-through (sc1) stores, drains them (every
-// wave's vmcnt(0), a barrier) and sets the tile's flag (sc1 store); the second polls that flag (sc1 loads; the first
-// is resident and waits for nothing), reads the partial by sc1 loads, adds it (one fp32 add per element: the same bits
-// whichever half finishes first), resets ticket and flag for the next launch and runs the epilogue. The hand-off is
-// MI355X_MICROARCH's first valid row (sc1 stores, drained, one flag per storing workgroup, sc1 loads). Partial slots
-// hold the accumulator layout (each lane's 32 f32x4 as consecutive 1 KiB wave rows). Deterministic, not bit-identical
-// to the unsplit kernels (two partial sums instead of one chain).
-template <int EPI, int FE>
-__global__ __launch_bounds__(512, 2) void gemm8h_kernel(GemmK p) {
-  extern __shared__ __attribute__((aligned(16))) char gsm[];
-  __shared__ int s_ticket;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  int bid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  }
-  const int tile = bid >> 1, half = bid & 1;
-  const int per_batch = p.tiles_m * p.tiles_n;
-  const int bz = tile / per_batch, rem = tile - bz * per_batch;
-  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
-  const int row0 = tm * 256, col0 = tn * 256;
-  const int nk = p.K / 64, kh = nk >> 1;
-  f32x4 acc[8][4];
-  pp8::mainloop(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, half ? kh : 0,
-                half ? nk - kh : kh, acc, gsm, wave, lane);
-  raw_barrier();  // (wave row 0 finished one segment earlier)
-  // (an opaque zero: nothing of the hand-off is computed before the main loop, where it would stay live and spill)
-  int z = 0;
-  asm volatile("" : "+s"(z));
-  int* ticket = p.sk_flag + tile + z;
-  int* flag = p.sk_flag + p.sk_batch + tile + z;  // (sk_batch: the number of tiles, the tickets' length)
-  const __amdgpu_buffer_rsrc_t rpart =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.sk_part + z), (short)0, 0x7fffffff, 0x00020000);
-  const uint32_t lane_off = (uint32_t)((wave * 32 * 64 + lane + z) * 16);
-  const uint32_t sbase = (uint32_t)(tile + z) * (8u * 32u * 64u * 16u);
-  if (tid == 0) s_ticket = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (s_ticket == 0) {  // first half done: publish the partial
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rpart,
-                                               lane_off + (uint32_t)((mi * 4 + ni) * 1024), sbase, 16 /* sc1 */);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    raw_barrier();
-    if (tid == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (tid == 0) {
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
-  }
-  raw_barrier();
-#pragma unroll
-  for (int m2 = 0; m2 < 8; m2 += 2) {  // two row blocks at a time (32 VGPRs in flight beside the accumulators)
-    f32x4 v[2][4];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        v[mi][ni] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rpart, lane_off + (uint32_t)(((m2 + mi) * 4 + ni) * 1024),
-                                                         sbase, 16 /* sc1 */));
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[m2 + mi][ni] = acc[m2 + mi][ni] + v[mi][ni];
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (tid == 0) {
-    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
-}
-
 template <int EPI, int FE, int DBG = 0>
 int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
   GemmK g = k0;
@@ -2135,57 +2050,8 @@ int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
   return 0;
 }
 
-template <int EPI, int FE>
-int launch_gemm8h_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s, long long T) {
-  GemmK g = k0;
-  g.tiles_m = (a->M + 255) / 256;
-  g.tiles_n = (a->N + 255) / 256;
-  g.sk_batch = (int)T;
-  g.sk_part = (float*)a->workspace;
-  g.sk_flag = (int*)((char*)a->workspace + (size_t)T * 262144);
-  constexpr int LDS = 2 * ph8::BUF;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8h_kernel<EPI, FE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm8h_kernel<EPI, FE>), dim3((unsigned)(2 * T)), dim3(512), LDS, s, g);
-  OCTSAM_LAUNCH_CHECK("octsam_gemm");
-  return 0;
-}
-
 static int g_small_oneshot = 1;  // K <= 256 small problems on gemm_small_kernel (fast path bit 65536 turns it off)
 static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
-
-static int sk_grid() {  // CUs of the current device
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (n_cu <= 0) n_cu = 256;
-  }
-  return n_cu;
-}
-constexpr long long WS_BYTES = 192LL << 20;  // octsam_gemm_workspace_bytes: up to 768 split tiles
-
-// the split-K-by-two form where it fills the waves better: deep K (>= 1536: the partial round trip is small beside
-// a half tile's main loop) and half-tile waves 10 % shorter than whole-tile waves; -1: not taken
-template <int EPI>
-int launch_gemm8h(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
-  const int G = sk_grid();
-  const long long T = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
-  const long long w1 = (T + G - 1) / G, w2 = (2 * T + G - 1) / G;
-  if (a->K < 1536 || (a->K / 64) < 4 || !(0.55 * (double)w2 < (double)w1) || a->workspace == nullptr ||
-      a->workspace_bytes < T * (262144 + 8) || ((uintptr_t)a->workspace & 255) != 0 || T > (1LL << 20))
-    return -1;
-  switch (k.fast_epi) {
-    case 1: return launch_gemm8h_fe<EPI, 1>(k, a, s, T);
-    case 2: return launch_gemm8h_fe<EPI, 2>(k, a, s, T);
-    case 4: return launch_gemm8h_fe<EPI, 4>(k, a, s, T);
-    default: return -1;
-  }
-}
 
 // kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
 template <int EPI>
@@ -2677,7 +2543,6 @@ static int g_rgroup = 1;  // rgroup_tm ordering (fast path bit 2048 turns it off
 static int g_res_lds = 1;  // gemm8 fp32 residual kind through LDS (fast path bit 4096 turns it off: A/B)
 static int g_gemm8w = 1;   // ping-pong kernel (gemm8w) for the shapes gemm8 takes (fast path bit 8192 turns it off: A/B)
 static int g_gemm8w4 = 0;  // ... and for those gemm4w takes (fast path bit 16384 turns it on: A/B)
-static int g_gemm8s = 1;   // its split-K-by-two form where the tiles quantise badly (fast path bit 32768 turns it off)
 template <int EPI>
 int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
   switch (k.fast_epi) {
@@ -3064,14 +2929,12 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_res_lds = (enable & 4096) ? 0 : 1;
   g_gemm8w = (enable & 8192) ? 0 : 1;
   g_gemm8w4 = (enable & 16384) ? 1 : 0;
-  g_gemm8s = (enable & 32768) ? 0 : 1;
   g_pp_skip = (enable >> 20) & 7;
   g_small_oneshot = (enable & 65536) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
 extern "C" int32_t octsam_gemm_last_path(void) { return t_last_path; }
-extern "C" int64_t octsam_gemm_workspace_bytes(void) { return WS_BYTES; }
 extern "C" int octsam_gemm_debug_stamps(int64_t* host, int32_t n_wg) {
   OCTSAM_CHECK_ARG(host && n_wg > 0 && n_wg <= STAMP_WG, "octsam_gemm_debug_stamps: bad args");
   const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n_wg * 4 * sizeof(long long));
@@ -3157,7 +3020,9 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
     const long long t256 = (long long)((a->M + 255) / 256) * ((a->N + 255) / 256) * a->batch;
     if (am <= 1 && bm <= 1 && a->a_blk == 0 && a->b_blk == 0 && t256 < 96 && t64 <= 4096 && g_small && !want_cs) {
       t_last_path = 3;
-      if (a->K <= 256 && g_small_oneshot) {
+      // (one-shot when its 64 KiB-LDS workgroups fit one wave of the chip at two per CU: N = 2048 measured slower,
+      //  13.2 vs 10.2 us, scripts/tok_gemm_ab.py)
+      if (a->K <= 256 && g_small_oneshot && t64 <= 512) {
         if (am == 0 && bm == 0) return launch_small<0, 0>(k, a->batch, s);
         if (am == 0 && bm == 1) return launch_small<0, 1>(k, a->batch, s);
         if (am == 1 && bm == 0) return launch_small<1, 0>(k, a->batch, s);
@@ -3219,11 +3084,6 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
                         (k.fast_epi == 1 || k.fast_epi == 2 || k.fast_epi == 4 || k.fast_epi == 8) &&
                         (a->act == 0 || a->act == OCTSAM_ACT_GELU) && (long long)a->M * a->lda * 2 < (1LL << 31) &&
                         (long long)a->N * a->ldb * 2 < (1LL << 31);
-      if (w_ok && g_gemm8s && (g_gemm8w4 || !(a->K <= 1024 && a->N <= 1024))) {
-        t_last_path = 2;
-        const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8h<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8h<0>(k, a, s);
-        if (r >= 0) return r;
-      }
       if (w_ok && g_gemm8w4) {
         t_last_path = 2;
         const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);

@@ -64,45 +64,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, M: int, N: int, K: int, out: torch
         b_blk=b_remap[0], b_rep=b_remap[1], r_blk=r_remap[0], r_rep=r_remap[1], k_total=k_total,
         c_rows=_mapped_rows(out, ldc, residual, ldr, pre_out) if row_map is not None else 0,
         a_colsum=ptr(a_colsum), b_colsum=ptr(b_colsum))
-    if (a_mode == 0 and b_mode == 0 and K >= 128 and K % 64 == 0 and A.dtype == e16 and
-            ((M + 255) // 256) * ((N + 255) // 256) * batch >= 256):  # (the shapes the stream-K form may take)
-        ws = _gemm_workspace(out.device)
-        args.workspace, args.workspace_bytes = ws.data_ptr(), ws.numel()
     _lib.call("octsam_gemm_f16" if e16 == torch.float16 else "octsam_gemm", ctypes.byref(args))
     return out
-
-
-_GEMM_WS = {}  # (device, stream, capture id) -> octsam_gemm's stream-K workspace (zero-filled, kept alive here)
-_HIP = None
-
-
-def _capture_id(stream: int) -> int:
-    """The HIP capture sequence id of a stream that is capturing (hipStreamGetCaptureInfo): unique per graph capture."""
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so")
-        _HIP.hipStreamGetCaptureInfo.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
-                                                 ctypes.POINTER(ctypes.c_ulonglong)]
-    status, cid = ctypes.c_int(0), ctypes.c_ulonglong(0)
-    rc = _HIP.hipStreamGetCaptureInfo(ctypes.c_void_p(stream), ctypes.byref(status), ctypes.byref(cid))
-    if rc != 0:
-        raise RuntimeError(f"hipStreamGetCaptureInfo failed ({rc})")
-    return int(cid.value)
-
-
-def _gemm_workspace(dev: torch.device) -> torch.Tensor:
-    """octsam_gemm's workspace for the current stream (octsam_gemm_args.workspace: the stream-K GEMM's partial tiles
-    and flags, zero-filled once; the kernels leave it zeroed). One per (device, stream) for eager launches, so two
-    streams never share one; inside a graph capture one per capture (allocated from the graph's pool, its zero fill
-    captured with it), so graphs replayed on different streams never share one either."""
-    stream = _lib.stream_handle()
-    cap = torch.cuda.is_current_stream_capturing()
-    key = (dev.index, stream, _capture_id(stream) if cap else 0)
-    ws = _GEMM_WS.get(key)
-    if ws is None:
-        ws = torch.zeros(int(_lib.load().octsam_gemm_workspace_bytes()), dtype=torch.uint8, device=dev)
-        _GEMM_WS[key] = ws
-    return ws
 
 
 def _span_rows(t: torch.Tensor, ld: int) -> int:

@@ -84,12 +84,6 @@ typedef struct octsam_gemm_args {
      the splits with octsam_splitk_reduce. */
   float* a_colsum;
   float* b_colsum;
-  /* device workspace of octsam_gemm_workspace_bytes() bytes (256-B aligned, zero-filled by the caller before its
-     first use; the kernels leave it zeroed again) or NULL: the split-K-by-two form of the ping-pong GEMM (deep K,
-     badly filled waves: the encoder's MLP2) keeps its fp32 partial tiles, tickets and flags there (ABI 24); without
-     it those GEMMs run unsplit. Two launches in flight at once (different streams) need different workspaces. */
-  void* workspace;
-  int64_t workspace_bytes;
 } octsam_gemm_args;
 
 int octsam_gemm(const octsam_gemm_args* args, void* stream);
@@ -105,9 +99,6 @@ void octsam_gemm_set_fast_path(int32_t enable);
    global_load_lds kernel, 2 8-phase / ping-pong / two-workgroup kernels, 3 small-problem kernel. Used to
    attribute per-kernel timings. */
 int32_t octsam_gemm_last_path(void);
-/* bytes of octsam_gemm_args.workspace (192 MiB: partial tiles of up to 768 split 256x256 tiles, their tickets and
-   flags) */
-int64_t octsam_gemm_workspace_bytes(void);
 /* diagnostics: fast path 9 runs the one-tile-per-workgroup 8-phase kernel with per-workgroup s_memtime stamps
    (entry, main loop done, epilogue stores done) and hardware ids; this copies the first n_wg workgroups' records
    (4 x int64 each: t0, t1, t2, XCC_ID << 32 | HW_ID) to host memory (synchronous) */
