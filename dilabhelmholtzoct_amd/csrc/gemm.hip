@@ -1879,8 +1879,9 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
 
   for (int t = 0; t < n; ++t) {
     const char* cur = gsm + (t & 1) * ph8::BUF;
-    // ---- L(t): DMA share, then the fragments of K-step t
-    constexpr bool DMA_IN_C = (SKIP & 8) != 0;
+    // ---- L(t): DMA share, then the fragments of K-step t (SKIP bit 16: the fragments first, then the DMA share)
+    constexpr bool DMA_IN_C = (SKIP & 8) != 0, READS_FIRST = (SKIP & 16) != 0;
+    auto issue_dma = [&]() {
     if ((SKIP & 1) || DMA_IN_C) {
     } else if (wr == 0) {
       if (t + 1 < n) {
@@ -1897,6 +1898,9 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
         for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
       }
     }
+    };
+    if constexpr ((SKIP & 32) != 0) __builtin_amdgcn_s_setprio(1);  // (bit 32: the loading wave at priority 1)
+    if (!READS_FIRST) issue_dma();
 #pragma unroll
     for (int kb = 0; kb < 2 && !(SKIP & 2); ++kb) {
 #pragma unroll
@@ -1904,6 +1908,7 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
     }
+    if (READS_FIRST) issue_dma();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (wr == 1 && DMA_IN_C) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A-lo(t+1), issued in C(t-1)
@@ -1913,6 +1918,7 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     raw_barrier();
+    if constexpr ((SKIP & 32) != 0) __builtin_amdgcn_s_setprio(0);
     // ---- C(t): the wave's 64 MFMAs
     if constexpr ((SKIP & 4) != 0) {
       if (t == 0)
@@ -2064,6 +2070,8 @@ int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool
       case 4: return launch_gemm8w_fe<EPI, 1, 20>(k, a, s);
       case 3: return launch_gemm8w_fe<EPI, 1, 19>(k, a, s);
       case 5: return launch_gemm8w_fe<EPI, 1, 24>(k, a, s);  // (fast path bits: 5 << 20 = DMA in the MFMA segment)
+      case 6: return launch_gemm8w_fe<EPI, 1, 32>(k, a, s);  // (6 << 20: fragments first, then the DMA share)
+      case 7: return launch_gemm8w_fe<EPI, 1, 64>(k, a, s);  // (7 << 20: that, with the loading wave at priority 1)
       default: return -1;
     }
   }

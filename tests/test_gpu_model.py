@@ -196,3 +196,35 @@ def test_attention_similarity(cuda, models, per_prompt):
     out = ours(image_embeddings=emb, input_boxes=boxes, attention_similarity=sim, multimask_output=True)
     with pytest.raises(NotImplementedError):
         out.pred_masks.float().sum().backward()
+
+
+@pytest.mark.parametrize("N", [3, 11])
+def test_decoder_backward_tok_group_bit_identical(cuda, models, N):
+    """The decoder backward with the token-side weight gradients deferred and issued as grouped launches
+    (MaskDecoder.tok_group, the default: octsam_wgrad_tok_group after the last in-place write they depend on,
+    _before_write) gives exactly the flat gradient of the one-launch-per-problem form (tok_group False), for a
+    small and a larger prompt count (the deferral's write-after-read guard)."""
+    ours, hf, _ = models
+    px, boxes, _ = _inputs(cuda, B=2, N=N, seed=11)
+    with torch.no_grad():
+        emb = hf.vision_encoder(px).last_hidden_state
+    dec = ours.mask_decoder
+    w = None
+    grads = []
+    prev = dec.tok_group
+    try:
+        for grouped in (True, False, True):
+            dec.tok_group = grouped
+            dec.flat.grad = None
+            out = ours(image_embeddings=emb, multimask_output=False, input_boxes=boxes)
+            if w is None:
+                w = torch.randn(out.pred_masks.shape, generator=torch.Generator().manual_seed(7)).to(cuda)
+            (out.pred_masks * w).sum().backward()
+            torch.cuda.synchronize()
+            grads.append(dec.flat.grad.detach().clone())
+    finally:
+        dec.tok_group = prev
+        dec.flat.grad = None
+    assert grads[0].abs().sum() > 0
+    assert torch.equal(grads[0], grads[1])
+    assert torch.equal(grads[0], grads[2])
