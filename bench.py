@@ -446,9 +446,14 @@ def val_protocol(args, device):
     state, adam = P.load_warm()
     runner = P.HipRunner(device, state, epoch_batches)
     pairs = []
-    for tr, va in P.SEEDS:
+    for idx, (tr, va) in enumerate(P.SEEDS):
+        if idx + 1 < len(P.SEEDS):  # the next pair's scans, synthesised on a host thread meanwhile
+            epoch_batches.prefetch(P.SEEDS[idx + 1][0], P.N_TRAIN)
+            epoch_batches.prefetch(P.SEEDS[idx + 1][1], P.N_VAL)
         hip = [round(P.dice_of(c), 5) for _, c in runner.run(state, adam, tr, va,
                                                               val_batches=epoch_batches(va, P.N_VAL, 0))]
+        epoch_batches.forget(tr, P.N_TRAIN)
+        epoch_batches.forget(va, P.N_VAL)
         g = gold_pairs[(tr, va)]
         pairs.append({"train_seed": tr, "val_seed": va, "hip": hip, "oracle": g["oracle_dice"],
                       "diff": [round(h - o, 5) for h, o in zip(hip, g["oracle_dice"])],

@@ -1829,7 +1829,8 @@ __device__ __forceinline__ void rd(e16x8& d, const char* base, int off) {
 // with the same barrier count (wave row 1 takes one extra at the start and skips the last); on return wave row 0 is
 // one segment ahead (its epilogue overlaps wave row 1's last MFMA cluster) and every LDS read of the loop is done.
 // SKIP (diagnostics, wrong results): bit 1 no DMA after the prologue, bit 2 no fragment reads, bit 4 no MFMAs;
-// bit 8: the DMA pieces are issued in the wave's MFMA segment (one after every 4 MFMAs) instead of its load segment
+// bit 8: the DMA pieces are issued in the wave's MFMA segment (one after every 4 MFMAs) instead of its load segment;
+// bit 16: the load segment issues its DMA share before its fragment reads
 template <bool ZACC = true, int SKIP = 0>  // ZACC: the first K-step's MFMAs start from zero (else from acc: zeroed)
 __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int kb0, int n,
                                          f32x4 (&acc)[8][4], char* gsm, int wave, int lane) {
@@ -1879,8 +1880,10 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
 
   for (int t = 0; t < n; ++t) {
     const char* cur = gsm + (t & 1) * ph8::BUF;
-    // ---- L(t): DMA share, then the fragments of K-step t (SKIP bit 16: the fragments first, then the DMA share)
-    constexpr bool DMA_IN_C = (SKIP & 8) != 0, READS_FIRST = (SKIP & 16) != 0;
+    // ---- L(t): the fragments of K-step t, then the DMA share, whose issue (~60+ cycles a piece) then overlaps the
+    // reads' latency instead of delaying them (qkv 120.6 -> 117.9 us, MLP2 (bf16 out) 134.7 -> 128.9,
+    // profiles/r06/gemm8w_rdfirst_ab.log; SKIP bit 16: the DMA share first, the first form, for A/B)
+    constexpr bool DMA_IN_C = (SKIP & 8) != 0, READS_FIRST = (SKIP & 16) == 0;
     auto issue_dma = [&]() {
     if ((SKIP & 1) || DMA_IN_C) {
     } else if (wr == 0) {
@@ -1899,7 +1902,6 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
       }
     }
     };
-    if constexpr ((SKIP & 32) != 0) __builtin_amdgcn_s_setprio(1);  // (bit 32: the loading wave at priority 1)
     if (!READS_FIRST) issue_dma();
 #pragma unroll
     for (int kb = 0; kb < 2 && !(SKIP & 2); ++kb) {
@@ -1918,7 +1920,6 @@ __device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     raw_barrier();
-    if constexpr ((SKIP & 32) != 0) __builtin_amdgcn_s_setprio(0);
     // ---- C(t): the wave's 64 MFMAs
     if constexpr ((SKIP & 4) != 0) {
       if (t == 0)
@@ -2070,8 +2071,7 @@ int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool
       case 4: return launch_gemm8w_fe<EPI, 1, 20>(k, a, s);
       case 3: return launch_gemm8w_fe<EPI, 1, 19>(k, a, s);
       case 5: return launch_gemm8w_fe<EPI, 1, 24>(k, a, s);  // (fast path bits: 5 << 20 = DMA in the MFMA segment)
-      case 6: return launch_gemm8w_fe<EPI, 1, 32>(k, a, s);  // (6 << 20: fragments first, then the DMA share)
-      case 7: return launch_gemm8w_fe<EPI, 1, 64>(k, a, s);  // (7 << 20: that, with the loading wave at priority 1)
+      case 6: return launch_gemm8w_fe<EPI, 1, 32>(k, a, s);  // (6 << 20: the DMA share before the fragments)
       default: return -1;
     }
   }

@@ -16,7 +16,7 @@ lib = _lib.load()
 VARIANTS = {"native": 1 | 8192 | 32768, "w": 1 | 32768, "split": 1, "w4": 1 | 16384,
             # diagnostics of the ping-pong loop (wrong results except dmac): no DMA / no fragment reads / no MFMAs
             "skipdma": 1 | (1 << 20), "skiprd": 1 | (2 << 20), "skipmfma": 1 | (4 << 20), "skipdmard": 1 | (3 << 20),
-            "dmac": 1 | (5 << 20), "rdfirst": 1 | (6 << 20), "rdfirst_prio": 1 | (7 << 20)}
+            "dmac": 1 | (5 << 20), "dmafirst": 1 | (6 << 20)}
 if os.environ.get("VARIANTS"):
     VARIANTS = {k: VARIANTS[k] for k in os.environ["VARIANTS"].split(",")}
 

@@ -52,8 +52,13 @@ def test_val_dice_parity_multiseed(cuda):
     rows = []
     for idx, (tr, va) in enumerate(P.SEEDS):
         g = gold_pairs[(tr, va)]
+        if idx + 1 < len(P.SEEDS):  # the next pair's scans, synthesised on a host thread meanwhile
+            epoch_batches.prefetch(P.SEEDS[idx + 1][0], P.N_TRAIN)
+            epoch_batches.prefetch(P.SEEDS[idx + 1][1], P.N_VAL)
         hip = [(k, P.dice_of(c)) for k, c in hip_runner.run(state, adam, tr, va,
                                                              val_batches=epoch_batches(va, P.N_VAL, 0))]
+        epoch_batches.forget(tr, P.N_TRAIN)
+        epoch_batches.forget(va, P.N_VAL)
         live = None
         if idx < P.LIVE_PAIRS:  # the oracle itself on this box, against its committed values
             ora_c, moved = runner.run(state, adam, tr, va)

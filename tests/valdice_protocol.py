@@ -210,13 +210,28 @@ def device_batches(device):
     from dilabhelmholtzoct_amd import data
     from dilabhelmholtzoct_amd.components import collate_device
     from dilabhelmholtzoct_amd.preprocess import DeviceProcessor
+    from concurrent.futures import ThreadPoolExecutor
     dproc = DeviceProcessor(device)
     raw = {}
+    pool = ThreadPoolExecutor(1)
+
+    def make_raw(seed, n):
+        ds = data.synthetic_oct(seed=seed, n=n)
+        return np.stack([np.array(d["image"]) for d in ds]), np.stack([np.array(d["label"]) for d in ds])
+
+    def prefetch(seed, n):
+        """Synthesise a later pair's scans on a host thread while the GPU trains the current pair."""
+        if (seed, n) not in raw:
+            raw[seed, n] = pool.submit(make_raw, seed, n)
+
+    def forget(seed, n):
+        raw.pop((seed, n), None)
 
     def epoch_batches(seed, n, epoch):
         if (seed, n) not in raw:
-            ds = data.synthetic_oct(seed=seed, n=n)
-            raw[seed, n] = (np.stack([np.array(d["image"]) for d in ds]), np.stack([np.array(d["label"]) for d in ds]))
+            raw[seed, n] = pool.submit(make_raw, seed, n)
+        if not isinstance(raw[seed, n], tuple):
+            raw[seed, n] = raw[seed, n].result()
         imgs, labs = raw[seed, n]
         out = []
         for s in range(0, n, BS):
@@ -226,6 +241,8 @@ def device_batches(device):
             b.pop("prompt_raw", None)
             out.append(b)
         return out
+    epoch_batches.prefetch = prefetch
+    epoch_batches.forget = forget
     return epoch_batches
 
 
