@@ -36,6 +36,7 @@ import valdice_protocol as P  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.timeout(900)  # 96 seed pairs: a few seconds each
 def test_val_dice_parity_multiseed(cuda):
     from oracle.eval_ref import mean_specificity_ref
     if not os.path.exists(P.WARM):
