@@ -1802,294 +1802,6 @@ int launch_gemm8_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Ping-pong 8-wave kernel (gemm8w): the same 256x256x64 tile, wave tiles (2 M x 4 N waves of 128 x 64), LDS
-// images and epilogues as gemm8, but each K-step of a wave is TWO segments between barriers instead of eight:
-//   L(t): the wave's 24 fragments of K-step t (8 A row blocks, 4 B column blocks, 2 k-halves; ds_read_b128 by
-//         inline asm into registers) plus its share of the LDS-DMA for later stages;
-//   C(t): all 64 of its 16x16x32 MFMAs of K-step t (1024 MFMA cycles, no LDS access).
-// The two wave rows run one segment apart (waves w and w+4 share a SIMD), so every segment pairs one wave's
-// matrix cluster with its SIMD partner's loads; gemm8's phases were 16 MFMAs (256 cycles) per barrier.
-// Stage t lives in buffer t & 1 ([A 256 x 64 | B 256 x 64] e16, 64 KiB); A rows 0-127 are read only by wave row
-// 0 (segment 2t), rows 128-255 only by wave row 1 (segment 2t+1), B by both, so each region is refilled as soon
-// as its last reader has passed a barrier, with the DMA split evenly over the loading waves:
-//   wave row 0 in L(t) (segment 2t):     B(t+1)                    -> landed at the end of its C(t): vmcnt(0)
-//   wave row 1 in L(t) (segment 2t+1):   A-hi(t+1), A-lo(t+2)      -> A-hi(t+1) landed at the end of its C(t)
-//                                                                     (vmcnt 4), A-lo(t+1) (issued in L(t-1))
-//                                                                     at the end of L(t) (vmcnt 8)
-//   prologue (all waves): stage 0 and A-lo(1).
-// Operands through buffer descriptors (rows past M / N read as zero); each 1 KiB DMA piece is 8 rows x 128 B, its
-// lane part of the offset depends only on the piece's parity (the chunk swizzle (r >> 1) & 7 of sw_off<64>).
-namespace pp8 {
-__device__ __forceinline__ void rd(e16x8& d, const char* base, int off) {
-  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(base + off)));
-}
-
-// The ping-pong main loop over K-steps [kb0, kb0 + n) of one 256x256 tile (n >= 1): acc = sum over those K-steps
-// (the first K-step's MFMAs start from zero). Stage t of the loop lives in buffer t & 1. Every wave enters and leaves
-// with the same barrier count (wave row 1 takes one extra at the start and skips the last); on return wave row 0 is
-// one segment ahead (its epilogue overlaps wave row 1's last MFMA cluster) and every LDS read of the loop is done.
-// SKIP (diagnostics, wrong results): bit 1 no DMA after the prologue, bit 2 no fragment reads, bit 4 no MFMAs;
-// bit 8: the DMA pieces are issued in the wave's MFMA segment (one after every 4 MFMAs) instead of its load segment;
-// bit 16: the load segment issues its DMA share before its fragment reads
-template <bool ZACC = true, int SKIP = 0>  // ZACC: the first K-step's MFMAs start from zero (else from acc: zeroed)
-__device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int kb0, int n,
-                                         f32x4 (&acc)[8][4], char* gsm, int wave, int lane) {
-  const int wr = wave >> 2, wc = wave & 3;
-  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(A + (long long)row0 * p.lda), (short)0, (p.M - row0) * lda2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(B + (long long)col0 * p.ldb), (short)0, (p.N - col0) * ldb2, 0x00020000);
-  uint32_t va[2], vb[2];  // lane part of a DMA piece's offset (by the piece's parity: the chunk swizzle of sw_off<64>)
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-    va[e] = (uint32_t)(r * lda2 + c * 16);
-    vb[e] = (uint32_t)(r * ldb2 + c * 16);
-  }
-  // piece j (8 rows) of A rows [h*128, h*128+128) / of B, loop stage t (K-step kb0 + t) into buffer t & 1
-  auto dma_a = [&](int h, int j, int t) {
-    char* dst = gsm + (t & 1) * ph8::BUF + (h * 128 + j * 8) * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)dst, 16, va[j & 1],
-                                             (h * 128 + (j & ~1) * 8) * lda2 + (kb0 + t) * 128, 0, 0);
-  };
-  auto dma_b = [&](int j, int t) {
-    char* dst = gsm + (t & 1) * ph8::BUF + 32768 + j * 8 * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1],
-                                             (j & ~1) * 8 * ldb2 + (kb0 + t) * 128, 0, 0);
-  };
-  e16x8 af[8][2], bf[4][2];
-  const int arow = wr * 128 + (lane & 15), brow = wc * 64 + (lane & 15), kq = lane >> 4;
-
-  // prologue: stage 0 (A-lo 2, A-hi 2, B 4 pieces per wave) and A-lo(1) (2 per wave)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 0);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) dma_a(1, wave * 2 + i, 0);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dma_b(wave * 4 + i, 0);
-  if (n > 1) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 1);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  raw_barrier();
-  if (wr == 1) raw_barrier();  // wave row 1 runs one segment behind
-
-  for (int t = 0; t < n; ++t) {
-    const char* cur = gsm + (t & 1) * ph8::BUF;
-    // ---- L(t): the fragments of K-step t, then the DMA share, whose issue (~60+ cycles a piece) then overlaps the
-    // reads' latency instead of delaying them (qkv 120.6 -> 117.9 us, MLP2 (bf16 out) 134.7 -> 128.9,
-    // profiles/r06/gemm8w_rdfirst_ab.log; SKIP bit 16: the DMA share first, the first form, for A/B)
-    constexpr bool DMA_IN_C = (SKIP & 8) != 0, READS_FIRST = (SKIP & 16) == 0;
-    auto issue_dma = [&]() {
-    if ((SKIP & 1) || DMA_IN_C) {
-    } else if (wr == 0) {
-      if (t + 1 < n) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dma_b(wc * 8 + i, t + 1);
-      }
-    } else {
-      if (t + 1 < n) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dma_a(1, wc * 4 + i, t + 1);
-      }
-      if (t + 2 < n) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
-      }
-    }
-    };
-    if (!READS_FIRST) issue_dma();
-#pragma unroll
-    for (int kb = 0; kb < 2 && !(SKIP & 2); ++kb) {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) rd(bf[ni][kb], cur + 32768, sw_off<64>(brow + ni * 16, kb * 4 + kq));
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
-    }
-    if (READS_FIRST) issue_dma();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (wr == 1 && DMA_IN_C) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A-lo(t+1), issued in C(t-1)
-    } else if (wr == 1) {  // A-lo(t+1), issued in L(t-1), before wave row 0 reads it in the next segment
-      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (t + 1 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    raw_barrier();
-    // ---- C(t): the wave's 64 MFMAs
-    if constexpr ((SKIP & 4) != 0) {
-      if (t == 0)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = __builtin_bit_cast(f32x4, af[mi][0]) + __builtin_bit_cast(f32x4, bf[ni][1]);
-    } else if (!DMA_IN_C && ZACC && t == 0) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
-    } else if (DMA_IN_C) {
-      // the wave's DMA share, one piece after every 4 MFMAs (sched_group_barrier: 4 MFMA, 1 VMEM)
-      const bool z = ZACC && t == 0;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], (z && kb == 0) ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
-          const int q = kb * 8 + mi;
-          if (q < 8) {
-            if (wr == 0) {
-              if (t + 1 < n) dma_b(wc * 8 + q, t + 1);
-            } else if (q < 4) {
-              if (t + 1 < n) dma_a(1, wc * 4 + q, t + 1);
-            } else {
-              if (t + 2 < n) dma_a(0, wc * 4 + q - 4, t + 2);
-            }
-          }
-        }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], acc[mi][ni], 0, 0, 0);
-    }
-    if (wr == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(t+1)
-      raw_barrier();
-    } else {
-      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t+1)
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (t + 1 < n) raw_barrier();
-    }
-  }
-}
-
-// the tile's epilogue (the lean kinds of epilogue_fast; the in-place fp32 residual through LDS, ph8::epilogue_res_lds,
-// in the LDS the main loop no longer reads)
-template <int EPI, int FE>
-__device__ __forceinline__ void epilogue(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0w, int col0w, char* gsm,
-                                         int wave, int lane) {
-  if constexpr (FE == 4) {
-    if (p.res_lds) {
-      char* bx = gsm + wave * 8192;
-      ph8::res_dma_q(p, bz, row0w, col0w, 0, bx, lane);
-      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0w, col0w, lane, bx, gsm + ph8::BUF + wave * 8192);
-      return;
-    }
-  }
-  if constexpr (FE == 1) {
-    ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0w, col0w, lane);
-  } else {
-    ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0w, col0w, lane);
-    ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0w, col0w, lane);
-  }
-}
-}  // namespace pp8
-
-// DBG 3 (diagnostics, fast path 9): per workgroup s_memtime at entry, at the end of wave row 0's and of wave row 1's
-// main loop and after the epilogue's stores (octsam_gemm_debug_stamps)
-template <int EPI, int FE, int DBG = 0>
-__global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
-  extern __shared__ __attribute__((aligned(16))) char gsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  long long st0 = 0;
-  if constexpr (DBG == 3) st0 = __builtin_amdgcn_s_memtime();
-  int bid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
-    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
-  }
-  const int per_batch = p.tiles_m * p.tiles_n;
-  const int bz = bid / per_batch, rem = bid - bz * per_batch;
-  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
-  const int row0 = tm * 256, col0 = tn * 256;
-  f32x4 acc[8][4];
-  pp8::mainloop<true, (DBG >= 16 ? DBG - 16 : 0)>(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0, col0, 0,
-                                                   p.K / 64, acc, gsm, wave, lane);
-  if constexpr (DBG == 3) {
-    const long long t1 = __builtin_amdgcn_s_memtime();
-    if ((wave & 3) == 0 && lane == 0 && blockIdx.x < STAMP_WG) g_stamps[4 * blockIdx.x + 1 + wr] = t1;
-  }
-  pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
-  if constexpr (DBG == 3) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const long long t2 = __builtin_amdgcn_s_memtime();
-    if (tid == 0 && blockIdx.x < STAMP_WG) {
-      g_stamps[4 * blockIdx.x] = st0;
-      g_stamps[4 * blockIdx.x + 3] = t2;
-    }
-  }
-}
-
-template <int EPI, int FE, int DBG = 0>
-int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
-  GemmK g = k0;
-  g.tiles_m = (a->M + 255) / 256;
-  g.tiles_n = (a->N + 255) / 256;
-  constexpr int LDS = 2 * ph8::BUF;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8w_kernel<EPI, FE, DBG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS);
-    attr = true;
-  }
-  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
-  hipLaunchKernelGGL((gemm8w_kernel<EPI, FE, DBG>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
-  OCTSAM_LAUNCH_CHECK("octsam_gemm");
-  return 0;
-}
-
-static int g_small_oneshot = 1;  // K <= 256 small problems on gemm_small_kernel (fast path bit 65536 turns it off)
-static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
-
-// kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
-template <int EPI>
-int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool stamped = false) {
-  if (g_pp_skip) {  // (diagnostics: the main loop without DMA / fragment reads / MFMAs; wrong results)
-    if (k.fast_epi != 1) return -1;
-    switch (g_pp_skip) {
-      case 1: return launch_gemm8w_fe<EPI, 1, 17>(k, a, s);
-      case 2: return launch_gemm8w_fe<EPI, 1, 18>(k, a, s);
-      case 4: return launch_gemm8w_fe<EPI, 1, 20>(k, a, s);
-      case 3: return launch_gemm8w_fe<EPI, 1, 19>(k, a, s);
-      case 5: return launch_gemm8w_fe<EPI, 1, 24>(k, a, s);  // (fast path bits: 5 << 20 = DMA in the MFMA segment)
-      case 6: return launch_gemm8w_fe<EPI, 1, 32>(k, a, s);  // (6 << 20: the DMA share before the fragments)
-      default: return -1;
-    }
-  }
-  if (stamped) {  // (diagnostics)
-    if (k.fast_epi == 1) return launch_gemm8w_fe<EPI, 1, 3>(k, a, s);
-    if (k.fast_epi == 4) return launch_gemm8w_fe<EPI, 4, 3>(k, a, s);
-    return -1;
-  }
-  switch (k.fast_epi) {
-    case 1: return launch_gemm8w_fe<EPI, 1>(k, a, s);
-    case 2: return launch_gemm8w_fe<EPI, 2>(k, a, s);
-    case 4: return launch_gemm8w_fe<EPI, 4>(k, a, s);
-    case 8: return launch_gemm8w_fe<EPI, 8>(k, a, s);
-    default: return -1;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // 256x192 variant of the 8-phase kernel for GEMMs whose 256-column tiles quantise badly on the chip (MLP2 /
 // proj at M = 32768, N = 768: 384 tiles = 1.5 waves of 256 CUs -> 512 tiles of 3/4 the work = 2 full waves).
 // Same phases, barriers and stagger; each wave owns 128 x 48 (3 column blocks of 16): Q(., 0) covers blocks
@@ -2225,6 +1937,310 @@ __device__ __forceinline__ void epilogue_n192(const GemmK& p, f32x4 (&acc)[8][3]
   }
 }
 }  // namespace ph8
+
+// ------------------------------------------------------------------------------------------------
+// Ping-pong 8-wave kernel (gemm8w): the same 256x256x64 tile, wave tiles (2 M x 4 N waves of 128 x 64), LDS
+// images and epilogues as gemm8, but each K-step of a wave is TWO segments between barriers instead of eight:
+//   L(t): the wave's 24 fragments of K-step t (8 A row blocks, 4 B column blocks, 2 k-halves; ds_read_b128 by
+//         inline asm into registers) plus its share of the LDS-DMA for later stages;
+//   C(t): all 64 of its 16x16x32 MFMAs of K-step t (1024 MFMA cycles, no LDS access).
+// The two wave rows run one segment apart (waves w and w+4 share a SIMD), so every segment pairs one wave's
+// matrix cluster with its SIMD partner's loads; gemm8's phases were 16 MFMAs (256 cycles) per barrier.
+// Stage t lives in buffer t & 1 ([A 256 x 64 | B 256 x 64] e16, 64 KiB); A rows 0-127 are read only by wave row
+// 0 (segment 2t), rows 128-255 only by wave row 1 (segment 2t+1), B by both, so each region is refilled as soon
+// as its last reader has passed a barrier, with the DMA split evenly over the loading waves:
+//   wave row 0 in L(t) (segment 2t):     B(t+1)                    -> landed at the end of its C(t): vmcnt(0)
+//   wave row 1 in L(t) (segment 2t+1):   A-hi(t+1), A-lo(t+2)      -> A-hi(t+1) landed at the end of its C(t)
+//                                                                     (vmcnt 4), A-lo(t+1) (issued in L(t-1))
+//                                                                     at the end of L(t) (vmcnt 8)
+//   prologue (all waves): stage 0 and A-lo(1).
+// Operands through buffer descriptors (rows past M / N read as zero); each 1 KiB DMA piece is 8 rows x 128 B, its
+// lane part of the offset depends only on the piece's parity (the chunk swizzle (r >> 1) & 7 of sw_off<64>).
+namespace pp8 {
+__device__ __forceinline__ void rd(e16x8& d, const char* base, int off) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(base + off)));
+}
+
+// The ping-pong main loop over K-steps [kb0, kb0 + n) of one 256x256 tile (n >= 1): acc = sum over those K-steps
+// (the first K-step's MFMAs start from zero). Stage t of the loop lives in buffer t & 1. Every wave enters and leaves
+// with the same barrier count (wave row 1 takes one extra at the start and skips the last); on return wave row 0 is
+// one segment ahead (its epilogue overlaps wave row 1's last MFMA cluster) and every LDS read of the loop is done.
+// SKIP (diagnostics, wrong results): bit 1 no DMA after the prologue, bit 2 no fragment reads, bit 4 no MFMAs;
+// bit 8: the DMA pieces are issued in the wave's MFMA segment (one after every 4 MFMAs) instead of its load segment;
+// bit 16: the load segment issues its DMA share before its fragment reads
+// NB: 16-column blocks per wave (4: the 256x256 tile; 3: 256x192, B 192 rows x 64 k per stage, 2 * NB DMA pieces per
+// wave of row 0 per K-step instead of 8; every wait count is unchanged, wave row 0 waits for all of its pieces)
+template <bool ZACC = true, int SKIP = 0, int NB = 4>  // ZACC: the first K-step's MFMAs start from zero (else from acc: zeroed)
+__device__ __forceinline__ void mainloop(const GemmK& p, const e16* A, const e16* B, int row0, int col0, int kb0, int n,
+                                         f32x4 (&acc)[8][NB], char* gsm, int wave, int lane) {
+  static_assert(NB == 3 || NB == 4, "gemm8w: 256- or 192-column tiles");
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + (long long)row0 * p.lda), (short)0, (p.M - row0) * lda2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B + (long long)col0 * p.ldb), (short)0, (p.N - col0) * ldb2, 0x00020000);
+  uint32_t va[2], vb[2];  // lane part of a DMA piece's offset (by the piece's parity: the chunk swizzle of sw_off<64>)
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int r = e * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+    va[e] = (uint32_t)(r * lda2 + c * 16);
+    vb[e] = (uint32_t)(r * ldb2 + c * 16);
+  }
+  // piece j (8 rows) of A rows [h*128, h*128+128) / of B, loop stage t (K-step kb0 + t) into buffer t & 1
+  auto dma_a = [&](int h, int j, int t) {
+    char* dst = gsm + (t & 1) * ph8::BUF + (h * 128 + j * 8) * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)dst, 16, va[j & 1],
+                                             (h * 128 + (j & ~1) * 8) * lda2 + (kb0 + t) * 128, 0, 0);
+  };
+  auto dma_b = [&](int j, int t) {
+    char* dst = gsm + (t & 1) * ph8::BUF + 32768 + j * 8 * 128;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)dst, 16, vb[j & 1],
+                                             (j & ~1) * 8 * ldb2 + (kb0 + t) * 128, 0, 0);
+  };
+  e16x8 af[8][2], bf[NB][2];
+  const int arow = wr * 128 + (lane & 15), brow = wc * 16 * NB + (lane & 15), kq = lane >> 4;
+
+  // prologue: stage 0 (A-lo 2, A-hi 2, B NB pieces per wave) and A-lo(1) (2 per wave)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dma_a(1, wave * 2 + i, 0);
+#pragma unroll
+  for (int i = 0; i < NB; ++i) dma_b(wave * NB + i, 0);
+  if (n > 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma_a(0, wave * 2 + i, 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // wave row 1 runs one segment behind
+
+  for (int t = 0; t < n; ++t) {
+    const char* cur = gsm + (t & 1) * ph8::BUF;
+    // ---- L(t): the fragments of K-step t, then the DMA share, whose issue (~60+ cycles a piece) then overlaps the
+    // reads' latency instead of delaying them (qkv 120.6 -> 117.9 us, MLP2 (bf16 out) 134.7 -> 128.9,
+    // profiles/r06/gemm8w_rdfirst_ab.log; SKIP bit 16: the DMA share first, the first form, for A/B)
+    constexpr bool DMA_IN_C = (SKIP & 8) != 0, READS_FIRST = (SKIP & 16) == 0;
+    auto issue_dma = [&]() {
+    if ((SKIP & 1) || DMA_IN_C) {
+    } else if (wr == 0) {
+      if (t + 1 < n) {
+#pragma unroll
+        for (int i = 0; i < 2 * NB; ++i) dma_b(wc * 2 * NB + i, t + 1);
+      }
+    } else {
+      if (t + 1 < n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(1, wc * 4 + i, t + 1);
+      }
+      if (t + 2 < n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma_a(0, wc * 4 + i, t + 2);
+      }
+    }
+    };
+    if (!READS_FIRST) issue_dma();
+#pragma unroll
+    for (int kb = 0; kb < 2 && !(SKIP & 2); ++kb) {
+#pragma unroll
+      for (int ni = 0; ni < NB; ++ni) rd(bf[ni][kb], cur + 32768, sw_off<64>(brow + ni * 16, kb * 4 + kq));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rd(af[mi][kb], cur, sw_off<64>(arow + mi * 16, kb * 4 + kq));
+    }
+    if (READS_FIRST) issue_dma();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wr == 1 && DMA_IN_C) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A-lo(t+1), issued in C(t-1)
+    } else if (wr == 1) {  // A-lo(t+1), issued in L(t-1), before wave row 0 reads it in the next segment
+      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (t + 1 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    // ---- C(t): the wave's 64 MFMAs
+    if constexpr ((SKIP & 4) != 0) {
+      if (t == 0)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni) acc[mi][ni] = __builtin_bit_cast(f32x4, af[mi][0]) + __builtin_bit_cast(f32x4, bf[ni][1]);
+    } else if (!DMA_IN_C && ZACC && t == 0) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], kb == 0 ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
+    } else if (DMA_IN_C) {
+      // the wave's DMA share, one piece after every 4 MFMAs (sched_group_barrier: 4 MFMA, 1 VMEM)
+      const bool z = ZACC && t == 0;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni)
+            acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], (z && kb == 0) ? (f32x4)0.0f : acc[mi][ni], 0, 0, 0);
+          const int q = kb * 8 + mi;
+          if (q < 8) {
+            if (wr == 0) {
+              if (t + 1 < n && q < 2 * NB) dma_b(wc * 2 * NB + q, t + 1);
+            } else if (q < 4) {
+              if (t + 1 < n) dma_a(1, wc * 4 + q, t + 1);
+            } else {
+              if (t + 2 < n) dma_a(0, wc * 4 + q - 4, t + 2);
+            }
+          }
+        }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NB; ++ni) acc[mi][ni] = mma16(bf[ni][kb], af[mi][kb], acc[mi][ni], 0, 0, 0);
+    }
+    if (wr == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(t+1)
+      raw_barrier();
+    } else {
+      if (t + 2 < n) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t+1)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t + 1 < n) raw_barrier();
+    }
+  }
+}
+
+// the tile's epilogue (the lean kinds of epilogue_fast; the in-place fp32 residual through LDS, ph8::epilogue_res_lds,
+// in the LDS the main loop no longer reads)
+template <int EPI, int FE>
+__device__ __forceinline__ void epilogue(const GemmK& p, f32x4 (&acc)[8][4], int bz, int row0w, int col0w, char* gsm,
+                                         int wave, int lane) {
+  if constexpr (FE == 4) {
+    if (p.res_lds) {
+      char* bx = gsm + wave * 8192;
+      ph8::res_dma_q(p, bz, row0w, col0w, 0, bx, lane);
+      ph8::epilogue_res_lds<EPI>(p, acc, bz, row0w, col0w, lane, bx, gsm + ph8::BUF + wave * 8192);
+      return;
+    }
+  }
+  if constexpr (FE == 1) {
+    ph8::epilogue_fast<EPI, FE, false>(p, acc, bz, row0w, col0w, lane);
+  } else {
+    ph8::epilogue_fast<EPI, FE, false, 0, 4>(p, acc, bz, row0w, col0w, lane);
+    ph8::epilogue_fast<EPI, FE, false, 4, 4>(p, acc, bz, row0w, col0w, lane);
+  }
+}
+}  // namespace pp8
+
+// DBG 3 (diagnostics, fast path 9): per workgroup s_memtime at entry, at the end of wave row 0's and of wave row 1's
+// main loop and after the epilogue's stores (octsam_gemm_debug_stamps)
+// NB = 3: 256x192 tiles (the 192-column main loop; the lean epilogue of a 128 x 48 wave tile, ph8::epilogue_n192)
+template <int EPI, int FE, int DBG = 0, int NB = 4>
+__global__ __launch_bounds__(512, 2) void gemm8w_kernel(GemmK p) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  long long st0 = 0;
+  if constexpr (DBG == 3) st0 = __builtin_amdgcn_s_memtime();
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + loc;
+  }
+  const int per_batch = p.tiles_m * p.tiles_n;
+  const int bz = bid / per_batch, rem = bid - bz * per_batch;
+  const int tm = rem / p.tiles_n, tn = rem - tm * p.tiles_n;
+  const int row0 = tm * 256, col0 = tn * 64 * NB;
+  f32x4 acc[8][NB];
+  pp8::mainloop<true, (DBG >= 16 ? DBG - 16 : 0), NB>(p, (const e16*)p.A + bz * p.sA, (const e16*)p.B + bz * p.sB, row0,
+                                                       col0, 0, p.K / 64, acc, gsm, wave, lane);
+  if constexpr (DBG == 3) {
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if ((wave & 3) == 0 && lane == 0 && blockIdx.x < STAMP_WG) g_stamps[4 * blockIdx.x + 1 + wr] = t1;
+  }
+  if constexpr (NB == 3) {
+    static_assert(FE == 1 || FE == 4, "gemm8w 192-column tiles: epilogue kinds 1 and 4");
+    if constexpr (FE == 1) {
+      ph8::epilogue_n192<EPI, FE, 0, 8>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+    } else {
+      ph8::epilogue_n192<EPI, FE, 0, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+      ph8::epilogue_n192<EPI, FE, 4, 4>(p, acc, bz, row0 + wr * 128, col0 + wc * 48, lane);
+    }
+  } else {
+    pp8::epilogue<EPI, FE>(p, acc, bz, row0 + wr * 128, col0 + wc * 64, gsm, wave, lane);
+  }
+  if constexpr (DBG == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const long long t2 = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && blockIdx.x < STAMP_WG) {
+      g_stamps[4 * blockIdx.x] = st0;
+      g_stamps[4 * blockIdx.x + 3] = t2;
+    }
+  }
+}
+
+template <int EPI, int FE, int DBG = 0, int NB = 4>
+int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) {
+  GemmK g = k0;
+  g.tiles_m = (a->M + 255) / 256;
+  g.tiles_n = NB == 4 ? (a->N + 255) / 256 : a->N / 192;  // (192: N % 192 == 0 host-checked)
+  constexpr int LDS = 2 * ph8::BUF;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8w_kernel<EPI, FE, DBG, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS);
+    attr = true;
+  }
+  const long long nwg = (long long)g.tiles_m * g.tiles_n * a->batch;
+  hipLaunchKernelGGL((gemm8w_kernel<EPI, FE, DBG, NB>), dim3((unsigned)nwg), dim3(512), LDS, s, g);
+  OCTSAM_LAUNCH_CHECK("octsam_gemm");
+  return 0;
+}
+
+static int g_small_oneshot = 1;  // K <= 256 small problems on gemm_small_kernel (fast path bit 65536 turns it off)
+static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
+static int g_n192w = 1;    // 256x192 ping-pong tiles where they fill the chip's waves better (fast path bit 131072: off)
+
+// kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
+template <int EPI>
+int launch_gemm8w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s, bool stamped = false) {
+  if (g_pp_skip) {  // (diagnostics: the main loop without DMA / fragment reads / MFMAs; wrong results)
+    if (k.fast_epi != 1) return -1;
+    switch (g_pp_skip) {
+      case 1: return launch_gemm8w_fe<EPI, 1, 17>(k, a, s);
+      case 2: return launch_gemm8w_fe<EPI, 1, 18>(k, a, s);
+      case 4: return launch_gemm8w_fe<EPI, 1, 20>(k, a, s);
+      case 3: return launch_gemm8w_fe<EPI, 1, 19>(k, a, s);
+      case 5: return launch_gemm8w_fe<EPI, 1, 24>(k, a, s);  // (fast path bits: 5 << 20 = DMA in the MFMA segment)
+      case 6: return launch_gemm8w_fe<EPI, 1, 32>(k, a, s);  // (6 << 20: the DMA share before the fragments)
+      default: return -1;
+    }
+  }
+  if (stamped) {  // (diagnostics)
+    if (k.fast_epi == 1) return launch_gemm8w_fe<EPI, 1, 3>(k, a, s);
+    if (k.fast_epi == 4) return launch_gemm8w_fe<EPI, 4, 3>(k, a, s);
+    return -1;
+  }
+  switch (k.fast_epi) {
+    case 1: return launch_gemm8w_fe<EPI, 1>(k, a, s);
+    case 2: return launch_gemm8w_fe<EPI, 2>(k, a, s);
+    case 4: return launch_gemm8w_fe<EPI, 4>(k, a, s);
+    case 8: return launch_gemm8w_fe<EPI, 8>(k, a, s);
+    default: return -1;
+  }
+}
+
 
 #define PH8_MFMA_N192(MH, NH, BF, NNI, FIRST)                                                            \
   __builtin_amdgcn_s_setprio(1);                                                                          \
@@ -2570,6 +2586,16 @@ int launch_gemm4w(const GemmK& k, const octsam_gemm_args* a, hipStream_t s) {
 // under the encoder lookahead (decoder kernels share the chip, quantisation stops mattering) the 256x256 tiles'
 // fewer epilogues win, 17.77 -> 17.43 ms/step (scripts/step_ab2.py, profiles/r02g/n192_ab.log)
 static int g_n192 = 0;
+inline int device_cus() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+  }
+  return n_cu;
+}
 inline bool prefer_n192(const octsam_gemm_args* a, int n_cu) {
   if (a->N % 192 != 0 || a->K < 64) return false;
   const long long tm = (a->M + 255) / 256;
@@ -2939,6 +2965,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_gemm8w4 = (enable & 16384) ? 1 : 0;
   g_pp_skip = (enable >> 20) & 7;
   g_small_oneshot = (enable & 65536) ? 0 : 1;
+  g_n192w = (enable & 131072) ? 0 : 1;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -3096,6 +3123,16 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
         t_last_path = 2;
         const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);
         if (r >= 0) return r;
+      }
+      // 256x192 ping-pong tiles where 256-column tiles quantise badly (N = 768: 384 tiles = 1.5 waves of 256 CUs, as
+      // 512 tiles of 3/4 the work = 2 full waves; QKV's N = 2304: 4.5 -> 6 x 3/4): MLP2, the projection, QKV
+      if (w_ok && g_gemm8w && g_n192w && g_use_glds == 1 && (k.fast_epi == 1 || k.fast_epi == 4) &&
+          a->row_map == nullptr && prefer_n192(a, device_cus())) {
+        t_last_path = 2;
+        if (a->act == OCTSAM_ACT_GELU)
+          return k.fast_epi == 1 ? launch_gemm8w_fe<OCTSAM_ACT_GELU, 1, 0, 3>(k, a, s)
+                                 : launch_gemm8w_fe<OCTSAM_ACT_GELU, 4, 0, 3>(k, a, s);
+        return k.fast_epi == 1 ? launch_gemm8w_fe<0, 1, 0, 3>(k, a, s) : launch_gemm8w_fe<0, 4, 0, 3>(k, a, s);
       }
       if (g_gemm4w && g_use_glds == 1 && a->K % 32 == 0 && a->K >= 64 && a->K <= 1024 && a->N <= 1024 &&
           a->batch == 1 && am == 0 && bm == 0 &&

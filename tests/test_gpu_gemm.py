@@ -447,12 +447,17 @@ def test_gemm_small_path(cuda, a_mode, b_mode, shape):
     (5000, 520, 192, "f32_res", 0),      # ragged M and N
     (9000, 392, 320, "e16", 2),          # ragged, GELU
     (4500, 768, 128, "f32", 0),          # fp32 C, two K-steps
-    (8192, 768, 768, "f32_res_rowmap", 0)])
+    (8192, 768, 768, "f32_res_rowmap", 0),
+    (16384, 384, 256, "e16", 0),         # 256x192 tiles: N = 384 as two 192-column tiles
+    (8000, 768, 256, "f32_res", 0),      # 256x192 tiles, ragged M, register residual epilogue
+    (8192, 576, 320, "e16", 2)])         # 256x192 tiles with GELU
 def test_gemm8w_pingpong(cuda, M, N, K, kind, act):
     """The ping-pong 8-wave GEMM (gemm8w: two segments per K-step, the wave rows one segment apart; octsam_gemm's
-    default for the 256x256-tile shapes, fast path bit 8192 = the 8-phase gemm8 instead): against torch fp32,
-    bit-identical to the 8-phase kernel (both chain the same 16x16x32 MFMAs over K in the same order) and run to
-    run; the encoder's kinds (vit-b / vit-l shapes) and ragged tiles, the row-mapped residual kind."""
+    default for the 256x256-tile shapes, fast path bit 8192 = the 8-phase gemm8 instead; its 256x192-tile form where
+    256-column tiles quantise badly — MLP2, QKV, N = 384 / 576 here — fast path bit 131072 = 256-column tiles only):
+    against torch fp32, bit-identical to the 8-phase kernel and across tile widths (all chain the same 16x16x32 MFMAs
+    over K in the same order) and run to run; the encoder's kinds (vit-b / vit-l shapes) and ragged tiles, the
+    row-mapped residual kind."""
     from dilabhelmholtzoct_amd import _lib, kernels
     lib = _lib.load()
     g = torch.Generator().manual_seed(M + 3 * N + 7 * K + act)
@@ -466,7 +471,7 @@ def test_gemm8w_pingpong(cuda, M, N, K, kind, act):
         perm[::7] = -1
         rmap = perm.to(cuda)
     outs = []
-    for fast in (1, 1, 1 | 8192):
+    for fast in (1, 1, 1 | 8192, 1 | 131072):
         lib.octsam_gemm_set_fast_path(fast | 256)
         if kind == "e16":
             out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
@@ -497,6 +502,7 @@ def test_gemm8w_pingpong(cuda, M, N, K, kind, act):
     assert _rel(outs[0], ref) < (8e-3 if kind == "e16" else 1e-5)
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[3])
 
 
 @pytest.mark.parametrize("am,bm", [(0, 0), (0, 1), (1, 0), (1, 1)])
