@@ -2210,7 +2210,11 @@ int launch_gemm8w_fe(const GemmK& k0, const octsam_gemm_args* a, hipStream_t s) 
 
 static int g_small_oneshot = 1;  // K <= 256 small problems on gemm_small_kernel (fast path bit 65536 turns it off)
 static int g_pp_skip = 0;  // diagnostics (fast path bits 0x100000 << {0,1,2}): gemm8w main loop parts skipped
-static int g_n192w = 1;    // 256x192 ping-pong tiles where they fill the chip's waves better (fast path bit 131072: off)
+// 256x192 ping-pong tiles where they fill the chip's waves better (fast path bit 262144 turns them on): opt-in, since
+// in the step they lose although they win in isolation — MLP2 163.9 -> 154.2 us, projection 63.7 -> 60.7 (QKV 121.7
+// -> 123.9), but the pipelined step 16.00 -> 16.48 ms and the sequential 18.19 -> 18.27 (profiles/r06/n192w_ab.log,
+// n192w_step_ab.log): the 1.5-wave 256x256 launches leave half the chip to the decoder stream in their last wave
+static int g_n192w = 0;
 
 // kinds of the ping-pong kernel (-1: not built for this kind, the caller takes gemm8)
 template <int EPI>
@@ -2965,7 +2969,7 @@ extern "C" void octsam_gemm_set_fast_path(int32_t enable) {
   g_gemm8w4 = (enable & 16384) ? 1 : 0;
   g_pp_skip = (enable >> 20) & 7;
   g_small_oneshot = (enable & 65536) ? 0 : 1;
-  g_n192w = (enable & 131072) ? 0 : 1;
+  g_n192w = (enable & 262144) ? 1 : 0;
   g_use_glds = enable & 255;
   g_n192 = g_use_glds == 24 ? 1 : 0;
 }
@@ -3124,8 +3128,8 @@ extern "C" int OCTSAM_GEMM_ENTRY(const octsam_gemm_args* a, void* stream) {
         const int r = a->act == OCTSAM_ACT_GELU ? launch_gemm8w<OCTSAM_ACT_GELU>(k, a, s) : launch_gemm8w<0>(k, a, s);
         if (r >= 0) return r;
       }
-      // 256x192 ping-pong tiles where 256-column tiles quantise badly (N = 768: 384 tiles = 1.5 waves of 256 CUs, as
-      // 512 tiles of 3/4 the work = 2 full waves; QKV's N = 2304: 4.5 -> 6 x 3/4): MLP2, the projection, QKV
+      // (opt-in) 256x192 ping-pong tiles where 256-column tiles quantise badly (N = 768: 384 tiles = 1.5 waves of 256
+      // CUs, as 512 tiles of 3/4 the work = 2 full waves; QKV's N = 2304: 4.5 -> 6 x 3/4): MLP2, the projection, QKV
       if (w_ok && g_gemm8w && g_n192w && g_use_glds == 1 && (k.fast_epi == 1 || k.fast_epi == 4) &&
           a->row_map == nullptr && prefer_n192(a, device_cus())) {
         t_last_path = 2;

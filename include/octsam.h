@@ -91,9 +91,10 @@ int octsam_gemm(const octsam_gemm_args* args, void* stream);
  * BASELINE configs[4] (sam-vit-huge, fp16) */
 int octsam_gemm_f16(const octsam_gemm_args* args, void* stream);
 /* enable (1, default) / disable (0) the persistent LDS-DMA 256x256 fast path of octsam_gemm (A/B testing);
-   bit 256 disables the small-problem tile kernel, bit 512 the two-workgroups-per-CU 256x128 kernel. Every path is a
-   hand-written kernel of this library (ABI 24: the hipBLASLt path of ABI 23 and its octsam_gemm_set_workspace are
-   gone). */
+   bit 256 disables the small-problem tile kernel, bit 512 the two-workgroups-per-CU 256x128 kernel, bit 8192 the
+   ping-pong 256x256 kernel (the 8-phase one instead), bit 65536 the one-shot small-K kernel; bit 262144 turns on the
+   opt-in 256x192 ping-pong tiles. Every path is a hand-written kernel of this library (ABI 24: the hipBLASLt path of
+   ABI 23 and its octsam_gemm_set_workspace are gone). */
 void octsam_gemm_set_fast_path(int32_t enable);
 /* which kernel the calling thread's last octsam_gemm launched: 0 generic tile kernel, 1 persistent
    global_load_lds kernel, 2 8-phase / ping-pong / two-workgroup kernels, 3 small-problem kernel. Used to

@@ -1,5 +1,5 @@
 """A/B of the ping-pong 8-wave GEMM (gemm8w, the default; fast path bit 8192 = the 8-phase kernel; bit 16384 also for
-the shapes gemm4w takes; bit 131072 = 256-column tiles only, no 256x192 form)
+the shapes gemm4w takes; bit 262144 = the opt-in 256x192 tiles where they fill the waves better)
 against the 8-phase / two-workgroup kernels on the encoder and decoder shapes (B = 8 images):
 interleaved rounds in one process (min of 5 rounds x 20 launches), outputs compared bitwise against the native
 default and in relative error against torch fp32. Diagnostic only."""
@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dilabhelmholtzoct_amd import _lib, kernels as K  # noqa: E402
 
 lib = _lib.load()
-VARIANTS = {"native": 1, "w256": 1 | 131072, "gemm8": 1 | 8192, "w4": 1 | 16384,
+VARIANTS = {"native": 1, "n192": 1 | 262144, "gemm8": 1 | 8192, "w4": 1 | 16384,
             # diagnostics of the ping-pong loop (wrong results except dmac): no DMA / no fragment reads / no MFMAs
             "skipdma": 1 | (1 << 20), "skiprd": 1 | (2 << 20), "skipmfma": 1 | (4 << 20), "skipdmard": 1 | (3 << 20),
             "dmac": 1 | (5 << 20), "dmafirst": 1 | (6 << 20)}

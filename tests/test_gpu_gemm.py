@@ -453,8 +453,8 @@ def test_gemm_small_path(cuda, a_mode, b_mode, shape):
     (8192, 576, 320, "e16", 2)])         # 256x192 tiles with GELU
 def test_gemm8w_pingpong(cuda, M, N, K, kind, act):
     """The ping-pong 8-wave GEMM (gemm8w: two segments per K-step, the wave rows one segment apart; octsam_gemm's
-    default for the 256x256-tile shapes, fast path bit 8192 = the 8-phase gemm8 instead; its 256x192-tile form where
-    256-column tiles quantise badly — MLP2, QKV, N = 384 / 576 here — fast path bit 131072 = 256-column tiles only):
+    default for the 256x256-tile shapes, fast path bit 8192 = the 8-phase gemm8 instead; fast path bit 262144 = its
+    opt-in 256x192-tile form where 256-column tiles quantise badly — MLP2, QKV, N = 384 / 576 here):
     against torch fp32, bit-identical to the 8-phase kernel and across tile widths (all chain the same 16x16x32 MFMAs
     over K in the same order) and run to run; the encoder's kinds (vit-b / vit-l shapes) and ragged tiles, the
     row-mapped residual kind."""
@@ -471,7 +471,7 @@ def test_gemm8w_pingpong(cuda, M, N, K, kind, act):
         perm[::7] = -1
         rmap = perm.to(cuda)
     outs = []
-    for fast in (1, 1, 1 | 8192, 1 | 131072):
+    for fast in (1, 1, 1 | 8192, 1 | 262144):
         lib.octsam_gemm_set_fast_path(fast | 256)
         if kind == "e16":
             out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
