@@ -215,7 +215,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ 
 // loop), one 32x32x16 MFMA per 16 rows; the NW partial tiles (and column sums) are added in fixed wave order
 // through LDS. Replaces the split-K tile GEMM + its reduction + the bias column-sum kernel + its reduction.
 namespace tok {
-constexpr int NST = 4;                    // ring stages per wave
+constexpr int NST = 4;                    // ring stages per wave (4-wave workgroups: 64 KiB, two per CU)
+#ifndef OCTSAM_TOK_NST8
+#define OCTSAM_TOK_NST8 2
+#endif
+// ring stages per wave of the 8-wave form (M > 1024 rows; 4 stages = 128 KiB, one workgroup per CU; 2 = 64 KiB, two
+// per CU: step 18.30 -> 18.24 ms sequential, 16.17 -> 16.14 pipelined, profiles/r06/tok_nst2_step_ab.log)
+template <int NW> constexpr int nst() { return NW == 8 ? OCTSAM_TOK_NST8 : NST; }
 constexpr int OPB = SROWS * 32 * 2;       // bytes of one operand per stage (2 KiB)
 constexpr int STB = 2 * OPB;              // stage bytes (A then B)
 
@@ -234,6 +240,7 @@ __device__ __forceinline__ void tok_tile(const bf16* __restrict__ dy, long long 
                                          long long ldx, long long M, int tile, int tiles_i, float* __restrict__ out,
                                          int ldo, float beta, float* __restrict__ db, char* smem) {
   using namespace tok;
+  constexpr int NST = tok::nst<NW>();
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int to = tile / tiles_i, ti = tile - to * tiles_i;
   const int o0 = to * 32, i0 = ti * 32;
@@ -385,7 +392,7 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
   const int tiles = (O / 32) * (I / 32);
   hipStream_t s = (hipStream_t)stream;
   if (M > 1024) {
-    constexpr int NW = 8, LDS = NW * tok::NST * tok::STB;
+    constexpr int NW = 8, LDS = NW * tok::nst<8>() * tok::STB;
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)wgrad_tok_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -394,7 +401,7 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
     hipLaunchKernelGGL(wgrad_tok_kernel<NW>, dim3(tiles), dim3(NW * 64), LDS, s, (const bf16*)dy, (long long)ldy,
                        (const bf16*)x, (long long)ldx, (long long)M, I / 32, out, I, beta, db);
   } else {
-    constexpr int NW = 4, LDS = NW * tok::NST * tok::STB;
+    constexpr int NW = 4, LDS = NW * tok::nst<4>() * tok::STB;
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)wgrad_tok_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -410,7 +417,8 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
 template <int NW>
 void launch_tok_group(TokGroup& g, hipStream_t s) {
   for (int k = g.n + 1; k <= TOK_GROUP_MAX; ++k) g.start[k] = g.start[g.n];
-  constexpr int LDS = NW * tok::NST * tok::STB;
+  constexpr int LDS = NW * tok::nst<NW>() * tok::STB;
+  static_assert(LDS >= NW * (1024 + 32) * 4, "the fixed-order reduction reuses the rings");
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)wgrad_tok_group_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
