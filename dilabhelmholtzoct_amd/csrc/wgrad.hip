@@ -315,6 +315,121 @@ __device__ __forceinline__ void tok_tile(const bf16* __restrict__ dy, long long 
   }
 }
 
+// one 64 x 64 output tile of one token-side problem (O, I multiples of 64): the same row partition over the NW waves,
+// stages of 32 rows, MFMA chain per 32x32 block and fixed-order wave sum as tok_tile, so every output element gets the
+// same bits as from the 32 x 32 tiles, while each dy / x column block read serves 64 outputs instead of 32 (the 32 x 32
+// tiles re-read the operands (O + I) / 32 times over, almost all of it past L2: 186 MB per grouped launch)
+namespace tok {
+constexpr int OPB64 = SROWS * 64 * 2;  // bytes of one operand per stage (4 KiB)
+constexpr int STB64 = 2 * OPB64;
+template <int NW> constexpr int nst64() { return 2; }
+template <int NW> constexpr int lds64() {
+  return NW * nst64<NW>() * STB64 > NW * (4096 + 64) * 4 ? NW * nst64<NW>() * STB64 : NW * (4096 + 64) * 4;
+}
+// one operand's stage, 64 columns: four 1 KiB loads (8-row groups; lane -> subtile lane >> 5, row (lane >> 2) & 7,
+// chunk lane & 3: stage_lane_off), the image of stage_load's layout at W = 64
+__device__ __forceinline__ void tok_load64(__amdgpu_buffer_rsrc_t rs, int voff, int soff, long long ld, char* lds) {
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(lds + 1024 * gq), 16, voff, soff + (int)(16 * ld * gq), 0,
+                                             0);
+}
+}  // namespace tok
+
+template <int NW>
+__device__ __forceinline__ void tok_tile64(const bf16* __restrict__ dy, long long ldy, const bf16* __restrict__ x,
+                                           long long ldx, long long M, int tile, int tiles_i, float* __restrict__ out,
+                                           int ldo, float beta, float* __restrict__ db, char* smem) {
+  using namespace tok;
+  constexpr int NST = tok::nst64<NW>();
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int to = tile / tiles_i, ti = tile - to * tiles_i;
+  const int o0 = to * 64, i0 = ti * 64;
+  const long long per = ((M + NW - 1) / NW + SROWS - 1) / SROWS * SROWS;
+  const long long m_beg = min(M, (long long)wave * per), m_end = min(M, m_beg + per);
+  const int nst = (int)((m_end - m_beg + SROWS - 1) / SROWS);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dy + m_beg * ldy + o0), (short)0, (int)((m_end - m_beg) * ldy * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + m_beg * ldx + i0), (short)0, (int)((m_end - m_beg) * ldx * 2), 0x00020000);
+  const int va = stage_lane_off(ldy, lane), vb = stage_lane_off(ldx, lane);
+  char* ring = smem + wave * NST * STB64;
+  const int fo = frag_lane_off<64>(lane);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.0f;
+  float cs[2] = {0.0f, 0.0f};
+  const bool want_cs = db != nullptr && ti == 0;
+  auto issue = [&](int s) {
+    char* st = ring + (s % NST) * STB64;
+    tok::tok_load64(ra, va, (int)(s * SROWS * ldy * 2), ldy, st);
+    tok::tok_load64(rb, vb, (int)(s * SROWS * ldx * 2), ldx, st + OPB64);
+  };
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nst) issue(s);
+  for (int s = 0; s < nst; ++s) {
+    if (s + NST - 1 < nst) {
+      issue(s + NST - 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (NST - 1)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* sg = ring + (s % NST) * STB64 + fo;
+#pragma unroll
+    for (int kk = 0; kk < SROWS / 16; ++kk) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = frag(sg, 2048 * kk + 512 * a);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bfr[b] = frag(sg + OPB64, 2048 * kk + 512 * b);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+      if (want_cs) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) cs[a] = frag_sum(af[a], cs[a]);
+      }
+    }
+  }
+  // fixed-order sum of the NW partial tiles (and column sums) through LDS (the rings are no longer read)
+  __syncthreads();
+  float* red = (float*)smem;  // [NW][4 blocks][16][64] accumulators, then [NW][64] column sums
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[((wave * 4 + 2 * a + b) * 16 + e) * 64 + lane] = acc[a][b][e];
+  if (want_cs) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const float v = cs[a] + __shfl_xor(cs[a], 32, 64);
+      if (lane < 32) red[NW * 4096 + wave * 64 + 32 * a + lane] = v;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < 4096; idx += NW * 64) {
+    const int blk = idx >> 10, e = (idx >> 6) & 15, l = idx & 63;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[((w * 4 + blk) * 16 + e) * 64 + l];
+    const int o = o0 + 32 * (blk >> 1) + (e & 3) + 8 * (e >> 2) + 4 * (l >> 5), i = i0 + 32 * (blk & 1) + (l & 31);
+    float* dst = out + (long long)o * ldo + i;
+    *dst = beta != 0.0f ? v + beta * *dst : v;
+  }
+  if (want_cs && tid < 64) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[NW * 4096 + w * 64 + tid];
+    db[o0 + tid] = v;
+  }
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restrict__ dy, long long ldy,
                                                             const bf16* __restrict__ x, long long ldx, long long M,
@@ -337,7 +452,11 @@ struct TokProb {
   long long ldy, ldx, M;
   int tiles_i, ldo;
   float beta;
+  int w64;  // 64 x 64 output tiles (O, I multiples of 64), else 32 x 32
 };
+#ifndef OCTSAM_TOK_W64
+#define OCTSAM_TOK_W64 1
+#endif
 struct TokGroup {
   TokProb p[TOK_GROUP_MAX];
   int start[TOK_GROUP_MAX + 1];
@@ -350,7 +469,10 @@ __global__ __launch_bounds__(NW * 64) void wgrad_tok_group_kernel(const TokGroup
   int k = 0;
   while (k + 1 < g.n && g.start[k + 1] <= b) ++k;
   const TokProb& q = g.p[k];
-  tok_tile<NW>(q.dy, q.ldy, q.x, q.ldx, q.M, b - g.start[k], q.tiles_i, q.out, q.ldo, q.beta, q.db, smem);
+  if (q.w64)
+    tok_tile64<NW>(q.dy, q.ldy, q.x, q.ldx, q.M, b - g.start[k], q.tiles_i, q.out, q.ldo, q.beta, q.db, smem);
+  else
+    tok_tile<NW>(q.dy, q.ldy, q.x, q.ldx, q.M, b - g.start[k], q.tiles_i, q.out, q.ldo, q.beta, q.db, smem);
 }
 
 int n_workgroups(long long M, long long& rows_per) {
@@ -417,8 +539,9 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
 template <int NW>
 void launch_tok_group(TokGroup& g, hipStream_t s) {
   for (int k = g.n + 1; k <= TOK_GROUP_MAX; ++k) g.start[k] = g.start[g.n];
-  constexpr int LDS = NW * tok::nst<NW>() * tok::STB;
-  static_assert(LDS >= NW * (1024 + 32) * 4, "the fixed-order reduction reuses the rings");
+  constexpr int LDS32 = NW * tok::nst<NW>() * tok::STB, LDS64 = tok::lds64<NW>();
+  constexpr int LDS = LDS32 > LDS64 ? LDS32 : LDS64;
+  static_assert(LDS32 >= NW * (1024 + 32) * 4, "the fixed-order reduction reuses the rings");
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)wgrad_tok_group_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -447,9 +570,10 @@ extern "C" int octsam_wgrad_tok_group(int32_t n, const void* const* dy, const in
                          (long long)M[k] * ldy[k] * 2 < (1LL << 31) && (long long)M[k] * ldx[k] * 2 < (1LL << 31),
                      "octsam_wgrad_tok_group: problem %d: ldy / ldx multiples of 8, operands 16-B aligned", k);
     TokGroup& g = M[k] > 1024 ? g8 : g4;
+    const int tw = OCTSAM_TOK_W64 && O[k] % 64 == 0 && I[k] % 64 == 0 ? 64 : 32;
     g.p[g.n] = TokProb{(const bf16*)dy[k], (const bf16*)x[k], out[k], db[k], (long long)ldy[k], (long long)ldx[k],
-                       (long long)M[k], I[k] / 32, I[k], beta[k]};
-    g.start[g.n + 1] = g.start[g.n] + (O[k] / 32) * (I[k] / 32);
+                       (long long)M[k], I[k] / tw, I[k], beta[k], tw == 64 ? 1 : 0};
+    g.start[g.n + 1] = g.start[g.n] + (O[k] / tw) * (I[k] / tw);
     ++g.n;
   }
   if (g8.n) launch_tok_group<8>(g8, (hipStream_t)stream);
