@@ -214,6 +214,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_kernel(const bf16* __restrict__ 
 // wave-private 4-stage LDS-DMA ring (32 rows x 32 columns of each operand per stage, no workgroup barrier in the
 // loop), one 32x32x16 MFMA per 16 rows; the NW partial tiles (and column sums) are added in fixed wave order
 // through LDS. Replaces the split-K tile GEMM + its reduction + the bias column-sum kernel + its reduction.
+#ifndef OCTSAM_TOK_W64
+#define OCTSAM_TOK_W64 1
+#endif
 namespace tok {
 constexpr int NST = 4;                    // ring stages per wave (4-wave workgroups: 64 KiB, two per CU)
 #ifndef OCTSAM_TOK_NST8
@@ -431,6 +434,19 @@ __device__ __forceinline__ void tok_tile64(const bf16* __restrict__ dy, long lon
 }
 
 template <int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_tok64_kernel(const bf16* __restrict__ dy, long long ldy,
+                                                              const bf16* __restrict__ x, long long ldx, long long M,
+                                                              int tiles_i, float* __restrict__ out, int ldo, float beta,
+                                                              float* __restrict__ db) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tok_tile64<NW>(dy, ldy, x, ldx, M, blockIdx.x, tiles_i, out, ldo, beta, db, smem);
+}
+
+// 64 x 64 tiles for the larger problems (graph-replayed alone, scripts/tok_wgrad_time.py: MLP lin1's dW 12.1 -> 7.5
+// us, lin2's 9.5 -> 7.4), 32 x 32 tiles while 64 x 64 ones would leave most CUs idle (a 256 x 256 dW: 4.2 vs 7.0 us)
+inline bool tok_w64(int O, int I) { return OCTSAM_TOK_W64 && O % 64 == 0 && I % 64 == 0 && (O / 64) * (I / 64) >= 64; }
+
+template <int NW>
 __global__ __launch_bounds__(NW * 64) void wgrad_tok_kernel(const bf16* __restrict__ dy, long long ldy,
                                                             const bf16* __restrict__ x, long long ldx, long long M,
                                                             int tiles_i, float* __restrict__ out, int ldo, float beta,
@@ -452,11 +468,8 @@ struct TokProb {
   long long ldy, ldx, M;
   int tiles_i, ldo;
   float beta;
-  int w64;  // 64 x 64 output tiles (O, I multiples of 64), else 32 x 32
+  int w64;  // 64 x 64 output tiles (tok_w64), else 32 x 32
 };
-#ifndef OCTSAM_TOK_W64
-#define OCTSAM_TOK_W64 1
-#endif
 struct TokGroup {
   TokProb p[TOK_GROUP_MAX];
   int start[TOK_GROUP_MAX + 1];
@@ -513,6 +526,30 @@ extern "C" int octsam_wgrad_tok(const void* dy, int64_t ldy, const void* x, int6
                    "octsam_wgrad_tok: ldy / ldx multiples of 8, operands 16-B aligned");
   const int tiles = (O / 32) * (I / 32);
   hipStream_t s = (hipStream_t)stream;
+  if (tok_w64(O, I)) {
+    const int t64 = (O / 64) * (I / 64);
+    if (M > 1024) {
+      constexpr int NW = 8, LDS = tok::lds64<NW>();
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)wgrad_tok64_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        attr = true;
+      }
+      hipLaunchKernelGGL(wgrad_tok64_kernel<NW>, dim3(t64), dim3(NW * 64), LDS, s, (const bf16*)dy, (long long)ldy,
+                         (const bf16*)x, (long long)ldx, (long long)M, I / 64, out, I, beta, db);
+    } else {
+      constexpr int NW = 4, LDS = tok::lds64<NW>();
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)wgrad_tok64_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        attr = true;
+      }
+      hipLaunchKernelGGL(wgrad_tok64_kernel<NW>, dim3(t64), dim3(NW * 64), LDS, s, (const bf16*)dy, (long long)ldy,
+                         (const bf16*)x, (long long)ldx, (long long)M, I / 64, out, I, beta, db);
+    }
+    OCTSAM_LAUNCH_CHECK("octsam_wgrad_tok");
+    return 0;
+  }
   if (M > 1024) {
     constexpr int NW = 8, LDS = NW * tok::nst<8>() * tok::STB;
     static bool attr = false;
@@ -570,7 +607,7 @@ extern "C" int octsam_wgrad_tok_group(int32_t n, const void* const* dy, const in
                          (long long)M[k] * ldy[k] * 2 < (1LL << 31) && (long long)M[k] * ldx[k] * 2 < (1LL << 31),
                      "octsam_wgrad_tok_group: problem %d: ldy / ldx multiples of 8, operands 16-B aligned", k);
     TokGroup& g = M[k] > 1024 ? g8 : g4;
-    const int tw = OCTSAM_TOK_W64 && O[k] % 64 == 0 && I[k] % 64 == 0 ? 64 : 32;
+    const int tw = tok_w64(O[k], I[k]) ? 64 : 32;
     g.p[g.n] = TokProb{(const bf16*)dy[k], (const bf16*)x[k], out[k], db[k], (long long)ldy[k], (long long)ldx[k],
                        (long long)M[k], I[k] / tw, I[k], beta[k], tw == 64 ? 1 : 0};
     g.start[g.n + 1] = g.start[g.n] + (O[k] / tw) * (I[k] / tw);

@@ -300,6 +300,10 @@ class MaskDecoder(nn.Module):
     # accumulations), and so does an in-place write into a tensor a pending problem reads (_before_write: d s4, which
     # each block's projection backward accumulates into once its out_proj backward has read it).
     tok_group = True
+    # flush the deferred group at the end of every two-way block as well (its operands still warm in L2 / MALL) instead
+    # of only when a group is full or blocked: pipelined 15.85 -> 15.71 ms, sequential 18.08 -> 18.08
+    # (scripts/step_ab3.py, profiles/r06/tok_flush_ab.log; one launch per weight instead: 15.77 / 18.17)
+    tok_flush_block = True
     _tok_pending = None
 
     @staticmethod
@@ -882,6 +886,8 @@ class MaskDecoder(nn.Module):
                 K.axpby(dq, dqin, dq)
                 K.axpby(dtok, dqin, dtok)
                 self._lin_bwd(dvs, ls.sa_vin_b, sa + "v_proj.weight", sa + "v_proj.bias", R, dx_out=dq, dx_beta=1.0)
+            if self.tok_flush_block and self._tok_pending:
+                self._flush_tok()
         # ---- token embeddings: d[iou_token; mask_tokens] = sum over prompts of d tokens[:, 0:5]
         gtok = self._group(self.flat_grad, ["iou_token.weight", "mask_tokens.weight"], 0)
         part = torch.empty(T * C, device=dev, dtype=f32)

@@ -10,8 +10,9 @@ tables, two workgroups per CU; n192 = octsam_gemm fast path 24 (256x192 tiles wh
 the [B, N, H, W] d-mask between them; t2isum_off = the first block's token->image backward per prompt +
 prompt group sums instead of octsam_dec_t2i_bwd_sum; dkeys_joint = the mask head's and the final attention's keys
 gradients as one product; dkeys_two = the two-product form; tokgroup_off = every token-side weight gradient as its own
-launch instead of the deferred grouped launches; blaslt_off = the encoder's MLP2 / projection / QKV on the 8-phase
-kernels instead of hipBLASLt, blaslt_qkv_off = only QKV back on them). Interleaved rounds, median of 5 rounds x 20 steps.
+launch instead of the deferred grouped launches; tokflush_block = the deferred group flushed at the end of every
+two-way block; n192w = the opt-in 256x192 ping-pong tiles; small_chained = the token-side K <= 256 products on the
+chained 64x64 kernel instead of the one-shot one). Interleaved rounds, median of 5 rounds x 20 steps.
 Diagnostic only."""
 import json
 import os
@@ -42,11 +43,8 @@ def main():
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
                 "dkeys_joint": ({}, {"fuse_dkeys": True}), "dkeys_two": ({}, {"fuse_dkeys": False}),
                 "tokgroup_off": ({}, {"tok_group": False}), "g4w_off": ({}, {}),
-                "blaslt_off": ({}, {}), "blaslt_qkv_off": ({}, {}),
-                "blaslt_tok_off": ({}, {})}
-    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512, "blaslt_off": 1 | 65536,
-            "blaslt_qkv_off": 1 | 131072,
-            "blaslt_tok_off": 1 | 262144}
+                "tokflush_block": ({}, {"tok_flush_block": True}), "n192w": ({}, {}), "small_chained": ({}, {})}
+    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512, "n192w": 1 | 262144, "small_chained": 1 | 65536}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
