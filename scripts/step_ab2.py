@@ -19,6 +19,10 @@ lib = _lib.load()
 args = argparse.Namespace(batch=8, prompt="bboxes")
 batch = data.to_device_batch(bench.make_batch(args, 0, device, data.make_processor()), device)
 model = SamModel.from_pretrained("facebook/sam-vit-base", seed=0).to(device)
+# DEC_ATTRS="name=value,..." sets mask-decoder attributes (A/B across processes, e.g. tok_flush_block=0)
+for kv in filter(None, os.environ.get("DEC_ATTRS", "").split(",")):
+    k, v = kv.split("=")
+    setattr(model.mask_decoder, k, bool(int(v)))
 K = 10
 best = {}
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):

@@ -43,8 +43,13 @@ def main():
                 "n192": ({}, {}), "t2isum_off": ({}, {"t2i_sum": False}),
                 "dkeys_joint": ({}, {"fuse_dkeys": True}), "dkeys_two": ({}, {"fuse_dkeys": False}),
                 "tokgroup_off": ({}, {"tok_group": False}), "g4w_off": ({}, {}),
-                "tokflush_block": ({}, {"tok_flush_block": True}), "n192w": ({}, {}), "small_chained": ({}, {})}
-    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512, "n192w": 1 | 262144, "small_chained": 1 | 65536}
+                "tokflush_block": ({}, {"tok_flush_block": True}), "n192w": ({}, {}), "small_chained": ({}, {}),
+                "default2": ({}, {}),
+                "combo": ({"fork_topo": False, "fused_pp": False}, {"fuse_dkeys": False}),
+                "combo_g4w": ({"fork_topo": False, "fused_pp": False}, {"fuse_dkeys": False}),
+                "topo_pp": ({"fork_topo": False, "fused_pp": False}, {})}
+    FAST = {"g4res_off": 1 | 1024 | 2048, "n192": 24, "g4w_off": 1 | 512, "n192w": 1 | 262144, "small_chained": 1 | 65536,
+            "combo_g4w": 1 | 512}
     ATTN = {"attn_v2": 2}  # global attention variant while capturing (-1: the library default)
     lib = _lib.load()
     for name in os.environ.get("STEP_VARIANTS", "default,wgrad_off").split(","):
