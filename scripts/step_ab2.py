@@ -29,6 +29,9 @@ for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for fp, pipe in variants:
         lib.octsam_gemm_set_fast_path(fp)
         st = FusedTrainStep(model, lr=0.0, topological=True, graphs=True, pipeline=bool(pipe))
+        for kv in filter(None, os.environ.get("STEP_ATTRS", "").split(",")):  # FusedTrainStep attributes, as DEC_ATTRS
+            k, v = kv.split("=")
+            setattr(st, k, bool(int(v)))
         for i in range(4):
             st.step(batch, next_batch=batch if i < 3 else None)
         st.flush()
