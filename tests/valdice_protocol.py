@@ -41,7 +41,9 @@ BS = 8
 EPOCHS = 4
 N_TRAIN, N_VAL = 128, 32
 WARM_STEPS, WARM_SEED, WARM_VAL_SEED = 64, 2000, 3000
-N_PAIRS = 96
+# OCTSAM_VALDICE_PAIRS: more pairs for a one-off resolution run (tests/golden/make_valdice_golden.py extends the
+# golden; test_gpu_val_dice.py and bench.py run the default 96)
+N_PAIRS = int(os.environ.get("OCTSAM_VALDICE_PAIRS", "96"))
 SEEDS = [(2000 + i, 3000 + i) for i in range(1, N_PAIRS + 1)]
 LIVE_PAIRS = 1  # tests/test_gpu_val_dice.py reruns the oracle live on the first LIVE_PAIRS pairs (against the golden)
 CHECKPOINTS = [0] + [(N_TRAIN // BS) * (e + 1) for e in range(EPOCHS)]
