@@ -466,10 +466,12 @@ def val_protocol(args, device):
     out = {"steps": P.CHECKPOINTS, "n_pairs": n, "mean_diff": mean_diff,
            "se": [v["se"] for v in verdict], "noise_floor_mean": [v.get("noise_floor_mean") for v in verdict],
            "max_abs_mean_diff": round(max(abs(d) for d in mean_diff), 5), "tolerance": P.TOL,
-           "within": bool(max(abs(d) for d in mean_diff) <= P.TOL), "checkpoints": verdict,
+           "within": bool(max(abs(d) for d in mean_diff) <= P.TOL),
+           "within_ci95": bool(all(v["ci_ok"] for v in verdict)), "checkpoints": verdict,
            "seconds": round(time.perf_counter() - t0, 1),
            "protocol": "tests/valdice_protocol.py (oracle-made warm start; per seed pair 4 epochs x 16 steps; 32 "
-                       "held-out scans; strict |mean over pairs of Dice_HIP - Dice_oracle| <= tolerance)",
+                       "held-out scans; strict |mean over pairs of Dice_HIP - Dice_oracle| <= tolerance; within_ci95: "
+                       "|mean| + 2 SE <= tolerance)",
            "oracle_source": "tests/golden/valdice_oracle.json", "pairs": pairs}
     log(f"val protocol: mean diff {mean_diff} ({out['seconds']} s)")
     torch.cuda.empty_cache()

@@ -12,12 +12,13 @@ oracle values depend on no HIP kernel. For every seed pair of valdice_protocol.S
   oracle_mode (bit-reproducible), scored by oracle/eval_ref.pooled_confusion_ref (training_utils.py:126-156): the
   committed values of tests/golden/valdice_oracle.json, and on the first LIVE_PAIRS pairs rerun live here.
 Asserted (valdice_protocol.mean_diff_verdict), strictly:
-* at EVERY checkpoint (steps 0, 16, 32, 48, 64), |mean over the N_PAIRS = 96 seed pairs of (Dice_HIP - Dice_oracle)|
-  <= 0.005. Past step 32 single trajectories are chaotic (the oracle's own Dice moves by up to 0.024 under
-  bf16-sized weight perturbations; per-pair differences reach 0.03-0.05 either way), which is why the comparison is a
-  mean over 96 independent pairs: its 2 standard errors (~0.003) stay inside the tolerance, and there is no
-  allowance for noise in the bound. The oracle's own perturbed-minus-base mean (one bf16-sized perturbation of the
-  start state per pair, from the golden) is printed beside it as the noise floor;
+* at EVERY checkpoint (steps 0, 16, 32, 48, 64), |mean over the N_PAIRS = 157 seed pairs of (Dice_HIP -
+  Dice_oracle)| <= 0.005, and the whole 95 % interval of that mean inside it: |mean| + 2 SE <= 0.005 (a bound that
+  gets harder, not easier, with fewer or noisier pairs). Past step 32 single trajectories are chaotic (the oracle's
+  own Dice moves by up to 0.05 under bf16-sized weight perturbations; per-pair differences reach 0.03-0.09 either
+  way), which is why the comparison is a mean over 157 independent pairs. The oracle's own perturbed-minus-base mean
+  (one bf16-sized perturbation of the start state per pair, from the golden) is printed beside it as the noise
+  floor;
 * the oracle is in the non-degenerate regime (mean specificity > 0.5), its Dice is a real segmentation (> 0.5) and the
   compared epochs trained (the oracle's decoder moved by more than 1 % in norm, its Dice changed);
 * the live oracle equals the committed golden (which bench.py quotes beside its own HIP run) within 1e-4 (same box
@@ -36,7 +37,7 @@ import valdice_protocol as P  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.timeout(900)  # 96 seed pairs: a few seconds each
+@pytest.mark.timeout(900)  # 157 seed pairs: under 2 s each (about 4.5 min)
 def test_val_dice_parity_multiseed(cuda):
     from oracle.eval_ref import mean_specificity_ref
     if not os.path.exists(P.WARM):
@@ -94,3 +95,5 @@ def test_val_dice_parity_multiseed(cuda):
         print(json.dumps(v))
     bad = [v for v in verdict if not v["ok"]]
     assert not bad, f"mean(Dice_HIP - Dice_oracle) outside the tolerance: {bad}"
+    wide = [v for v in verdict if not v["ci_ok"]]
+    assert not wide, f"the 95 % interval of mean(Dice_HIP - Dice_oracle) reaches past the tolerance: {wide}"
