@@ -454,6 +454,8 @@ def val_protocol(args, device):
                                                               val_batches=epoch_batches(va, P.N_VAL, 0))]
         epoch_batches.forget(tr, P.N_TRAIN)
         epoch_batches.forget(va, P.N_VAL)
+        if (idx + 1) % 16 == 0:
+            log(f"val protocol: {idx + 1}/{len(P.SEEDS)} pairs ({time.perf_counter() - t0:.0f} s)")
         g = gold_pairs[(tr, va)]
         pairs.append({"train_seed": tr, "val_seed": va, "hip": hip, "oracle": g["oracle_dice"],
                       "diff": [round(h - o, 5) for h, o in zip(hip, g["oracle_dice"])],

@@ -29,7 +29,6 @@ import os
 import sys
 
 import pytest
-import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import valdice_protocol as P  # noqa: E402
@@ -37,42 +36,63 @@ import valdice_protocol as P  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.timeout(900)  # 157 seed pairs: under 2 s each (about 4.5 min)
-def test_val_dice_parity_multiseed(cuda):
-    from oracle.eval_ref import mean_specificity_ref
+# the pairs run in CHUNKS tests (module-scoped runners, rows collected in order), so the test runner reports progress
+# every minute or so instead of staying silent for the whole protocol; the last test takes the verdict
+CHUNKS = 4
+
+
+@pytest.fixture(scope="module")
+def protocol(cuda):
     if not os.path.exists(P.WARM):
         pytest.fail(f"missing {P.WARM}: run tests/golden/make_valdice_golden.py --warm on the GPU box")
     if not os.path.exists(P.ORACLE_JSON):
         pytest.fail(f"missing {P.ORACLE_JSON}: run tests/golden/make_valdice_golden.py --oracle on the GPU box")
     state, adam = P.load_warm()
     gold_pairs = {(g["train_seed"], g["val_seed"]): g for g in json.load(open(P.ORACLE_JSON))["pairs"]}
+    epoch_batches = P.device_batches(cuda)
+    return {"state": state, "adam": adam, "gold": gold_pairs, "oracle": P.OracleRunner(cuda),
+            "batches": epoch_batches, "hip": P.HipRunner(cuda, state, epoch_batches), "rows": {}}
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("chunk", range(CHUNKS))
+def test_val_dice_pairs(protocol, chunk):
+    """Pairs chunk::CHUNKS... in order: the HIP run of each pair, and on the first LIVE_PAIRS pairs the oracle live."""
+    from oracle.eval_ref import mean_specificity_ref
+    gold_pairs, epoch_batches = protocol["gold"], protocol["batches"]
     missing = [p for p in P.SEEDS if p not in gold_pairs]
     assert not missing, f"golden lacks pairs {missing}: make_valdice_golden.py --oracle --keep"
-    runner = P.OracleRunner(cuda)
-    epoch_batches = P.device_batches(cuda)
-    hip_runner = P.HipRunner(cuda, state, epoch_batches)
-    rows = []
-    for idx, (tr, va) in enumerate(P.SEEDS):
+    n = len(P.SEEDS)
+    lo, hi = chunk * n // CHUNKS, (chunk + 1) * n // CHUNKS
+    for idx in range(lo, hi):
+        tr, va = P.SEEDS[idx]
         g = gold_pairs[(tr, va)]
-        if idx + 1 < len(P.SEEDS):  # the next pair's scans, synthesised on a host thread meanwhile
+        if idx + 1 < n:  # the next pair's scans, synthesised on a host thread meanwhile
             epoch_batches.prefetch(P.SEEDS[idx + 1][0], P.N_TRAIN)
             epoch_batches.prefetch(P.SEEDS[idx + 1][1], P.N_VAL)
-        hip = [(k, P.dice_of(c)) for k, c in hip_runner.run(state, adam, tr, va,
-                                                             val_batches=epoch_batches(va, P.N_VAL, 0))]
+        hip = [(k, P.dice_of(c)) for k, c in protocol["hip"].run(protocol["state"], protocol["adam"], tr, va,
+                                                                 val_batches=epoch_batches(va, P.N_VAL, 0))]
         epoch_batches.forget(tr, P.N_TRAIN)
         epoch_batches.forget(va, P.N_VAL)
         live = None
         if idx < P.LIVE_PAIRS:  # the oracle itself on this box, against its committed values
-            ora_c, moved = runner.run(state, adam, tr, va)
+            ora_c, moved = protocol["oracle"].run(protocol["state"], protocol["adam"], tr, va)
             live = [P.dice_of(c) for _, c in ora_c]
             spec = mean_specificity_ref(ora_c[-1][1])
-            runner.forget(tr, va)
+            protocol["oracle"].forget(tr, va)
         else:
             moved, spec = g["oracle_moved"], g["oracle_specificity"]
-        rows.append({"pair": (tr, va), "hip": [d for _, d in hip], "oracle": g["oracle_dice"], "live": live,
-                     "spec": spec, "moved": moved, "spread": g.get("spread"), "perturbed": P.perturbed_of(g)})
+        protocol["rows"][idx] = {"pair": (tr, va), "hip": [d for _, d in hip], "oracle": g["oracle_dice"],
+                                 "live": live, "spec": spec, "moved": moved, "spread": g.get("spread"),
+                                 "perturbed": P.perturbed_of(g)}
         print(f"pair {tr}/{va}: HIP {[round(d, 5) for _, d in hip]} oracle {g['oracle_dice']} diff "
               f"{[round(h - o, 5) for (_, h), o in zip(hip, g['oracle_dice'])]} spread {g.get('spread')}")
+
+
+def test_val_dice_parity_multiseed(protocol):
+    """The verdict over every pair (the chunks above must all have run)."""
+    assert sorted(protocol["rows"]) == list(range(len(P.SEEDS))), "run the test_val_dice_pairs chunks first"
+    rows = [protocol["rows"][i] for i in range(len(P.SEEDS))]
     n = len(rows)
     mean_diff = [sum(r["hip"][i] - r["oracle"][i] for r in rows) / n for i in range(len(P.CHECKPOINTS))]
     print("mean over pairs of Dice_HIP - Dice_oracle per checkpoint:", [f"{d:+.5f}" for d in mean_diff])
