@@ -37,8 +37,8 @@ pytestmark = pytest.mark.gpu
 
 
 # the pairs run in CHUNKS tests (module-scoped runners, rows collected in order), so the test runner reports progress
-# every minute or so instead of staying silent for the whole protocol; the last test takes the verdict
-CHUNKS = 4
+# every half minute or so instead of staying silent for the whole protocol; the last test takes the verdict
+CHUNKS = 12
 
 
 @pytest.fixture(scope="module")
@@ -52,6 +52,13 @@ def protocol(cuda):
     epoch_batches = P.device_batches(cuda)
     return {"state": state, "adam": adam, "gold": gold_pairs, "oracle": P.OracleRunner(cuda),
             "batches": epoch_batches, "hip": P.HipRunner(cuda, state, epoch_batches), "rows": {}}
+
+
+@pytest.mark.timeout(400)
+def test_val_dice_setup(protocol):
+    """The runners (graph capture of the HIP step, the fp32 oracle model) and the golden: every pair present."""
+    missing = [p for p in P.SEEDS if p not in protocol["gold"]]
+    assert not missing, f"golden lacks pairs {missing}: make_valdice_golden.py --oracle --keep"
 
 
 @pytest.mark.timeout(400)
