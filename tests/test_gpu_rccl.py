@@ -83,7 +83,7 @@ def test_bench_rccl_world1(cuda):
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "2",
            "--cpu-baseline", "0", "--val", "0", "--data-path", "0", "--e2e-steps", "0", "--topo-all", "0",
-           "--loop-images", "0", "--roof-steps", "0"]
+           "--loop-images", "0", "--roof-steps", "0", "--val-protocol", "0", "--top-off", "0"]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
